@@ -1,0 +1,42 @@
+// sm_internal.h -- launcher interfaces between the C-ABI layer (sm_api.hip) and the
+// kernels (sm_compress.hip, sm_decompress.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sm {
+
+// Batch descriptor: block b is in[in_off[b] .. +in_len[b]) -> out[out_off[b] ..).
+// All pointers are device pointers.
+struct CompressArgs {
+  const uint8_t* in;
+  const uint64_t* in_off;
+  const uint32_t* in_len;
+  uint8_t* out;
+  const uint64_t* out_off;
+  uint32_t* out_len;
+  uint32_t nblk;
+  uint32_t table_size;  // 0: per block from its length (internal.jl:107-113); else fixed (Q2)
+  int header;           // 1: prefix each block with varint(len) (independent snappy stream)
+};
+
+struct DecompressArgs {
+  const uint8_t* in;
+  const uint64_t* in_off;
+  const uint32_t* in_len;
+  uint8_t* out;
+  const uint64_t* out_off;
+  const uint32_t* out_cap;
+  uint32_t* out_len;
+  int32_t* status;
+  uint32_t nblk;
+};
+
+// mode 0 = reference (byte-identical to Snappy.jl), 1 = fast (wave-parallel parse)
+hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s);
+hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
+// concatenate per-fragment outputs into one stream after a varint header (single-buffer API)
+hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
+                         const uint64_t* dst_off, uint8_t* dst, uint32_t nblk, hipStream_t s);
+
+}  // namespace sm
