@@ -1,0 +1,115 @@
+/*
+ * snappy_mi355x.h -- C ABI of the MI355X (gfx950) snappy codec (libsnappy_mi355x.so).
+ *
+ * Drop-in boundary for krm01/Snappy.jl's hot path.  Every entry point names the reference
+ * interface it replaces (paths relative to the reference repo root).  The shape follows
+ * snappy-c.h, the C ABI the reference already ccalls in test/libsnappy.jl:5-30: caller
+ * allocates the output, sizes travel as size_t in/out.  INTEGRATION.md shows the Julia
+ * ccall binding a maintainer adds to src/Snappy.jl.
+ *
+ * Error model: the reference throws ErrorException(msg) (src/Snappy.jl:21,50,
+ * src/varint.jl:36, src/internal.jl:499,505,518).  Here each message has its own status
+ * code (16..21), sm_status_message() returns the reference's exact text, and codes 1/2 keep
+ * libsnappy's meaning (INVALID_INPUT, BUFFER_TOO_SMALL).
+ *
+ * Two compress modes:
+ *   SM_MODE_REFERENCE -- output byte-identical to Snappy.jl compress() (incl. its quirks);
+ *   SM_MODE_FAST      -- wave-parallel parse; any output decodes bit-exactly under
+ *                        Snappy.jl uncompress() and libsnappy, bytes differ from the reference.
+ * Decompression has one mode, with the reference's accept/reject behaviour.
+ *
+ * Threading: an sm_ctx owns one HIP device, one stream and its scratch; calls on one ctx
+ * must be serialised by the caller; distinct ctxs are independent.
+ */
+#ifndef SNAPPY_MI355X_H_
+#define SNAPPY_MI355X_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int32_t sm_status;
+enum {
+  SM_OK = 0,
+  SM_INVALID_INPUT = 1,        /* snappy-c.h SNAPPY_INVALID_INPUT (generic) */
+  SM_BUFFER_TOO_SMALL = 2,     /* snappy-c.h SNAPPY_BUFFER_TOO_SMALL */
+  SM_ERR_INPUT_TOO_LARGE = 16, /* "Input too large."                   src/Snappy.jl:21 */
+  SM_ERR_INVALID = 17,         /* "Invalid input."                     src/Snappy.jl:50 */
+  SM_ERR_VARINT = 18,          /* "Could not decode varint32."         src/varint.jl:36 */
+  SM_ERR_COPY_OFFSET = 19,     /* "Invalid input: corrupt copy offset" src/internal.jl:499 */
+  SM_ERR_COPY_LENGTH = 20,     /* "Invalid input: corrupt copy length" src/internal.jl:505 */
+  SM_ERR_LITERAL = 21,         /* "Invalid input: corrupt literal"     src/internal.jl:518 */
+  SM_ERR_DEVICE = 32,          /* HIP runtime failure / no device */
+  SM_ERR_ARGUMENT = 33         /* bad argument (NULL, block > 64 KiB in a batch, ...) */
+};
+
+enum { SM_MODE_REFERENCE = 0, SM_MODE_FAST = 1 };
+
+#define SM_BLOCK_SIZE 65536u /* src/internal.jl:31 K_BLOCK_SIZE */
+
+typedef struct sm_ctx sm_ctx;
+
+/* Reference text for a status code (the ErrorException message), or a description. */
+const char* sm_status_message(sm_status st);
+
+/* ---- format helpers (host, no device needed) ------------------------------------ */
+/* replaces maxlength_compressed, src/Snappy.jl:80-82 (= snappy_max_compressed_length) */
+size_t sm_max_compressed_length(size_t source_length);
+/* replaces length_uncompressed, src/Snappy.jl:90-92 (= snappy_uncompressed_length) */
+sm_status sm_uncompressed_length(const char* compressed, size_t compressed_length, size_t* result);
+/* replaces parse32, src/varint.jl:12-37.  off is 0-based; *next is 0-based. */
+sm_status sm_parse32(const uint8_t* buf, size_t len, size_t off, uint32_t* value, size_t* next);
+/* replaces encode32!, src/varint.jl:46-69.  Writes 1..5 bytes, returns the count. */
+size_t sm_encode32(uint8_t* buf, uint32_t value);
+
+/* ---- device context -------------------------------------------------------------- */
+sm_ctx* sm_ctx_create(int device);
+void sm_ctx_destroy(sm_ctx* ctx);
+/* the HIP stream the ctx launches on (hipStream_t) */
+void* sm_ctx_stream(sm_ctx* ctx);
+
+/* ---- single buffer, host memory (the reference's exported API) -------------------- */
+/* replaces compress(::Vector{UInt8}), src/Snappy.jl:20-36 (and compress(::String), :38).
+ * *compressed_length: in = capacity (>= sm_max_compressed_length(n)), out = bytes written. */
+sm_status sm_compress(sm_ctx* ctx, const char* input, size_t input_length, char* compressed,
+                      size_t* compressed_length, int mode);
+/* replaces uncompress(::Vector{UInt8}), src/Snappy.jl:46-52.
+ * *uncompressed_length: in = capacity, out = bytes written. */
+sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t compressed_length, char* uncompressed,
+                        size_t* uncompressed_length);
+
+/* ---- batched, device memory (the GPU hot path; asynchronous on `stream`) ----------------
+ * Block b: input d_in[d_in_off[b] .. +d_in_len[b]), d_in_len[b] <= 65536; each block becomes
+ * an independent snappy stream (varint header + one compress_fragment!, i.e. exactly
+ * compress(block) of src/Snappy.jl:20-36) written at d_out + d_out_off[b], which must have
+ * room for sm_max_compressed_length(d_in_len[b]) bytes.  d_out_len[b] receives its size
+ * (0xffffffff if the block was longer than 64 KiB).  stream: hipStream_t or NULL = ctx stream. */
+sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                   const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
+                                   const uint64_t* d_out_off, uint32_t* d_out_len, int mode, void* stream);
+/* Block b: compressed stream d_in[d_in_off[b] .. +d_in_len[b]) -> d_out + d_out_off[b] with
+ * capacity d_out_cap[b].  d_status[b] = SM_OK or the reference's error code (first error in
+ * stream order); d_out_len[b] = decoded bytes (0 on error).  Each block decodes as
+ * uncompress(block), src/Snappy.jl:46-52. */
+sm_status sm_uncompress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                     const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
+                                     const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                     uint32_t* d_out_len, int32_t* d_status, void* stream);
+
+/* ---- batched, host memory (H2D + kernel + D2H, synchronous) ------------------------ */
+sm_status sm_compress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                            uint32_t nblk, uint8_t* out, const uint64_t* out_off, uint32_t* out_len, int mode);
+sm_status sm_uncompress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                              uint32_t nblk, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                              uint32_t* out_len, int32_t* status);
+
+/* library build identification ("snappy_mi355x gfx950 <git-describe>") */
+const char* sm_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SNAPPY_MI355X_H_ */

@@ -1,0 +1,296 @@
+"""snappy.jl_amd -- MI355X-native Snappy codec with Snappy.jl's API surface.
+
+Host-side mirror of krm01/Snappy.jl (src/Snappy.jl:1-94) over the C ABI in
+include/snappy_mi355x.h (libsnappy_mi355x.so, hand-written gfx950 HIP kernels).
+
+    compress(x)            -> bytes     Snappy.jl compress(::Vector{UInt8}) / (::String)  :20,:38
+    uncompress(x)          -> bytes     Snappy.jl uncompress(::Vector{UInt8})            :46
+    maxlength_compressed(n)             Snappy.jl:80
+    length_uncompressed(x) -> (n, next) Snappy.jl:90  (next is a 0-based index here)
+    parse32(buf, off) / encode32(v)     src/varint.jl:12 / :46 (0-based offsets)
+
+Errors raise SnappyError carrying the reference's exact ErrorException message.
+`mode="reference"` (default) produces Snappy.jl's exact bytes; `mode="fast"` uses the
+wave-parallel parse (valid snappy, decodes bit-exactly, different bytes).
+
+Batched GPU path (the north-star hot path): compress_batch / uncompress_batch on host
+arrays, and compress_batch_device / uncompress_batch_device on torch tensors already
+resident in HBM.
+
+There is no CPU fallback: importing works without a GPU, but every codec call needs the
+HIP library and a device, and raises if either is missing.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsnappy_mi355x.so")
+BLOCK_SIZE = 65536
+
+SM_OK = 0
+SM_BUFFER_TOO_SMALL = 2
+MODES = {"reference": 0, "fast": 1}
+
+# exported symbols of include/snappy_mi355x.h (checked by tests/test_abi.py)
+ABI_SYMBOLS = (
+    "sm_status_message", "sm_max_compressed_length", "sm_uncompressed_length", "sm_parse32",
+    "sm_encode32", "sm_ctx_create", "sm_ctx_destroy", "sm_ctx_stream", "sm_compress", "sm_uncompress",
+    "sm_compress_batch_device", "sm_uncompress_batch_device", "sm_compress_batch",
+    "sm_uncompress_batch", "sm_version",
+)
+
+
+class SnappyError(Exception):
+    """Mirrors the ErrorException the reference throws; .code is the sm_status."""
+
+    def __init__(self, code, message=None):
+        self.code = int(code)
+        super().__init__(message if message is not None else status_message(code))
+
+
+_lib = None
+_ctx = {}
+
+
+def library_path():
+    return LIB_PATH
+
+
+def lib():
+    """Load libsnappy_mi355x.so (raises OSError if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError("libsnappy_mi355x.so not built (run __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, sz, i32, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_uint32
+        L.sm_status_message.restype = ctypes.c_char_p
+        L.sm_status_message.argtypes = [i32]
+        L.sm_max_compressed_length.restype = sz
+        L.sm_max_compressed_length.argtypes = [sz]
+        L.sm_uncompressed_length.restype = i32
+        L.sm_uncompressed_length.argtypes = [vp, sz, ctypes.POINTER(sz)]
+        L.sm_parse32.restype = i32
+        L.sm_parse32.argtypes = [vp, sz, sz, ctypes.POINTER(u32), ctypes.POINTER(sz)]
+        L.sm_encode32.restype = sz
+        L.sm_encode32.argtypes = [vp, u32]
+        L.sm_ctx_create.restype = vp
+        L.sm_ctx_create.argtypes = [ctypes.c_int]
+        L.sm_ctx_destroy.restype = None
+        L.sm_ctx_destroy.argtypes = [vp]
+        L.sm_ctx_stream.restype = vp
+        L.sm_ctx_stream.argtypes = [vp]
+        L.sm_compress.restype = i32
+        L.sm_compress.argtypes = [vp, vp, sz, vp, ctypes.POINTER(sz), ctypes.c_int]
+        L.sm_uncompress.restype = i32
+        L.sm_uncompress.argtypes = [vp, vp, sz, vp, ctypes.POINTER(sz)]
+        L.sm_compress_batch_device.restype = i32
+        L.sm_compress_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int, vp]
+        L.sm_uncompress_batch_device.restype = i32
+        L.sm_uncompress_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+        L.sm_compress_batch.restype = i32
+        L.sm_compress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
+        L.sm_uncompress_batch.restype = i32
+        L.sm_uncompress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+        L.sm_version.restype = ctypes.c_char_p
+        L.sm_version.argtypes = []
+        _lib = L
+    return _lib
+
+
+def status_message(code):
+    return lib().sm_status_message(int(code)).decode()
+
+
+def _bytes(x):
+    """Accept bytes / bytearray / memoryview / str / uint8 ndarray (String method, Snappy.jl:38)."""
+    if isinstance(x, str):
+        x = x.encode("utf-8")
+    if isinstance(x, np.ndarray):
+        return np.ascontiguousarray(x, dtype=np.uint8)
+    return np.frombuffer(bytes(x), dtype=np.uint8)
+
+
+def context(device=0):
+    """Per-device sm_ctx (one HIP stream + scratch).  Raises if no device is usable."""
+    c = _ctx.get(device)
+    if c is None:
+        c = lib().sm_ctx_create(device)
+        if not c:
+            raise SnappyError(32, "no usable HIP device %d for snappy_mi355x" % device)
+        _ctx[device] = c
+    return c
+
+
+def _mode(mode):
+    if mode not in MODES:
+        raise ValueError("mode must be 'reference' or 'fast'")
+    return MODES[mode]
+
+
+def maxlength_compressed(n):
+    """Snappy.jl:80-82."""
+    return lib().sm_max_compressed_length(int(n))
+
+
+def parse32(buf, offset=0):
+    """src/varint.jl:12-37 with a 0-based offset; returns (value, next_offset)."""
+    a = _bytes(buf)
+    v = ctypes.c_uint32(0)
+    nx = ctypes.c_size_t(0)
+    st = lib().sm_parse32(a.ctypes.data if a.size else None, a.size, int(offset), ctypes.byref(v), ctypes.byref(nx))
+    if st:
+        raise SnappyError(st)
+    return v.value, nx.value
+
+
+def encode32(value):
+    """src/varint.jl:46-69; returns the varint bytes."""
+    out = np.zeros(8, dtype=np.uint8)
+    n = lib().sm_encode32(out.ctypes.data, int(value))
+    return out[:n].tobytes()
+
+
+def length_uncompressed(data):
+    """Snappy.jl:90-92."""
+    return parse32(data, 0)
+
+
+def compress(data, mode="reference", device=0):
+    """Snappy.jl:20-36 (and the String method :38), computed on the GPU."""
+    src = _bytes(data)
+    if src.size > 0xFFFFFFFF:
+        raise SnappyError(16)
+    cap = maxlength_compressed(src.size)
+    out = np.empty(cap, dtype=np.uint8)
+    ol = ctypes.c_size_t(cap)
+    st = lib().sm_compress(context(device), src.ctypes.data if src.size else None, src.size, out.ctypes.data,
+                           ctypes.byref(ol), _mode(mode))
+    if st:
+        raise SnappyError(st)
+    return out[: ol.value].tobytes()
+
+
+def uncompress(data, device=0):
+    """Snappy.jl:46-52, computed on the GPU; raises SnappyError with the reference message."""
+    src = _bytes(data)
+    size, _ = length_uncompressed(src)
+    out = np.empty(max(size, 1), dtype=np.uint8)
+    ol = ctypes.c_size_t(size)
+    st = lib().sm_uncompress(context(device), src.ctypes.data if src.size else None, src.size, out.ctypes.data,
+                             ctypes.byref(ol))
+    if st:
+        raise SnappyError(st)
+    return out[: ol.value].tobytes()
+
+
+# ---- batched host API ---------------------------------------------------------------
+
+def pack_blocks(blocks):
+    """list of byte strings -> (packed u8 array, u64 offsets, u32 lengths)."""
+    lens = np.array([len(b) for b in blocks], dtype=np.uint32)
+    offs = np.zeros(len(blocks), dtype=np.uint64)
+    if len(blocks) > 1:
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(bytes(b) for b in blocks), dtype=np.uint8) if blocks else np.zeros(0, np.uint8)
+    return np.ascontiguousarray(buf), offs, lens
+
+
+def slot_offsets(in_len):
+    """Fixed output slots of max_compressed_length(len) bytes (16-B aligned)."""
+    caps = (32 + in_len.astype(np.uint64) + in_len.astype(np.uint64) // 6 + 15) // 16 * 16
+    offs = np.zeros(in_len.size, dtype=np.uint64)
+    if in_len.size > 1:
+        offs[1:] = np.cumsum(caps[:-1], dtype=np.uint64)
+    return offs, caps
+
+
+def compress_batch(blocks, mode="fast", device=0):
+    """Compress independent <=64 KiB blocks; returns a list of snappy streams (bytes)."""
+    buf, in_off, in_len = pack_blocks(blocks)
+    if np.any(in_len > BLOCK_SIZE):
+        raise ValueError("batch blocks must be <= 65536 bytes")
+    out_off, caps = slot_offsets(in_len)
+    out = np.empty(int(out_off[-1] + caps[-1]) if len(blocks) else 1, dtype=np.uint8)
+    out_len = np.zeros(len(blocks), dtype=np.uint32)
+    if not blocks:
+        return []
+    st = lib().sm_compress_batch(context(device), buf.ctypes.data, in_off.ctypes.data, in_len.ctypes.data,
+                                 len(blocks), out.ctypes.data, out_off.ctypes.data, out_len.ctypes.data,
+                                 _mode(mode))
+    if st:
+        raise SnappyError(st)
+    return [out[int(o): int(o) + int(l)].tobytes() for o, l in zip(out_off, out_len)]
+
+
+def uncompress_batch(streams, capacities=None, device=0):
+    """Decode independent snappy streams; returns (list of bytes-or-None, status array)."""
+    if not streams:
+        return [], np.zeros(0, np.int32)
+    buf, in_off, in_len = pack_blocks(streams)
+    if capacities is None:
+        caps = []
+        for s in streams:
+            try:
+                caps.append(parse32(s)[0])
+            except SnappyError:
+                caps.append(0)
+        capacities = caps
+    cap = np.array(capacities, dtype=np.uint32)
+    out_off = np.zeros(len(streams), dtype=np.uint64)
+    if len(streams) > 1:
+        out_off[1:] = np.cumsum(cap[:-1].astype(np.uint64), dtype=np.uint64)
+    out = np.empty(max(int(cap.astype(np.uint64).sum()), 1), dtype=np.uint8)
+    out_len = np.zeros(len(streams), dtype=np.uint32)
+    status = np.zeros(len(streams), dtype=np.int32)
+    st = lib().sm_uncompress_batch(context(device), buf.ctypes.data, in_off.ctypes.data, in_len.ctypes.data,
+                                   len(streams), out.ctypes.data, out_off.ctypes.data, cap.ctypes.data,
+                                   out_len.ctypes.data, status.ctypes.data)
+    if st:
+        raise SnappyError(st)
+    res = [out[int(o): int(o) + int(l)].tobytes() if s == 0 else None for o, l, s in zip(out_off, out_len, status)]
+    return res, status
+
+
+# ---- batched device API (torch tensors resident in HBM) -----------------------------
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def compress_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, mode="fast", stream=None,
+                          device=None):
+    """All arguments are torch CUDA tensors (uint8 / int64 / int32).  Asynchronous on `stream`
+    (a torch.cuda.Stream or raw hipStream_t int; default: torch's current stream)."""
+    import torch
+    dev = d_in.device.index if device is None else device
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    elif hasattr(stream, "cuda_stream"):
+        stream = stream.cuda_stream
+    st = lib().sm_compress_batch_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), d_in_len.numel(),
+                                        _ptr(d_out), _ptr(d_out_off), _ptr(d_out_len), _mode(mode),
+                                        ctypes.c_void_p(stream))
+    if st:
+        raise SnappyError(st)
+
+
+def uncompress_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_cap, d_out_len, d_status,
+                            stream=None, device=None):
+    import torch
+    dev = d_in.device.index if device is None else device
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    elif hasattr(stream, "cuda_stream"):
+        stream = stream.cuda_stream
+    st = lib().sm_uncompress_batch_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len),
+                                          d_in_len.numel(), _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
+                                          _ptr(d_out_len), _ptr(d_status), ctypes.c_void_p(stream))
+    if st:
+        raise SnappyError(st)
+
+
+def version():
+    return lib().sm_version().decode()

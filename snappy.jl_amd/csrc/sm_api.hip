@@ -1,0 +1,382 @@
+// sm_api.hip -- C ABI (include/snappy_mi355x.h) over the gfx950 kernels.
+// Host framing follows src/Snappy.jl:20-52: varint header, 64 KiB fragments sharing one
+// table size derived from the total length (quirk Q2), final produced==declared check (the
+// latter lives in the decode kernel).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <new>
+#include <vector>
+
+#include "../../include/snappy_mi355x.h"
+#include "sm_device.h"
+#include "sm_internal.h"
+
+#ifndef SM_VERSION_STR
+#define SM_VERSION_STR "dev"
+#endif
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n < 4096 ? 4096 : n;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct sm_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  DevBuf in, out, out2, meta;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+inline hipStream_t pick_stream(sm_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+#define SM_CHECK(x)                 \
+  do {                              \
+    if ((x) != hipSuccess) return SM_ERR_DEVICE; \
+  } while (0)
+
+extern "C" {
+
+const char* sm_status_message(sm_status st) {
+  switch (st) {
+    case SM_OK: return "OK";
+    case SM_INVALID_INPUT: return "Invalid input.";
+    case SM_BUFFER_TOO_SMALL: return "Buffer too small.";
+    case SM_ERR_INPUT_TOO_LARGE: return "Input too large.";
+    case SM_ERR_INVALID: return "Invalid input.";
+    case SM_ERR_VARINT: return "Could not decode varint32.";
+    case SM_ERR_COPY_OFFSET: return "Invalid input: corrupt copy offset";
+    case SM_ERR_COPY_LENGTH: return "Invalid input: corrupt copy length";
+    case SM_ERR_LITERAL: return "Invalid input: corrupt literal";
+    case SM_ERR_DEVICE: return "HIP device error.";
+    case SM_ERR_ARGUMENT: return "Invalid argument.";
+    default: return "Unknown status.";
+  }
+}
+
+const char* sm_version(void) { return "snappy_mi355x gfx950 " SM_VERSION_STR; }
+
+size_t sm_max_compressed_length(size_t n) { return 32 + n + n / 6; }
+
+sm_status sm_parse32(const uint8_t* buf, size_t len, size_t off, uint32_t* value, size_t* next) {
+  uint32_t result = 0;
+  for (int i = 0; i < 5; ++i) {
+    if (off + i >= len) return SM_ERR_VARINT;
+    uint32_t b = buf[off + i];
+    if (i < 4) {
+      result |= (b & 0x7f) << (7 * i);
+      if (b < 0x80) {
+        if (value) *value = result;
+        if (next) *next = off + i + 1;
+        return SM_OK;
+      }
+    } else {
+      result |= (b & 0x7f) << 28;
+      if (b < 0x10) {
+        if (value) *value = result;
+        if (next) *next = off + 5;
+        return SM_OK;
+      }
+    }
+  }
+  return SM_ERR_VARINT;
+}
+
+size_t sm_encode32(uint8_t* buf, uint32_t v) {
+  size_t i = 0;
+  while (v >= 0x80) {
+    buf[i++] = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  buf[i++] = (uint8_t)v;
+  return i;
+}
+
+sm_status sm_uncompressed_length(const char* compressed, size_t n, size_t* result) {
+  uint32_t v = 0;
+  sm_status st = sm_parse32((const uint8_t*)compressed, n, 0, &v, nullptr);
+  if (st == SM_OK && result) *result = v;
+  return st;
+}
+
+sm_ctx* sm_ctx_create(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0 || device < 0 || device >= count) return nullptr;
+  sm_ctx* ctx = new (std::nothrow) sm_ctx();
+  if (!ctx) return nullptr;
+  ctx->device = device;
+  DeviceGuard g(device);
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return nullptr;
+  }
+  return ctx;
+}
+
+void sm_ctx_destroy(sm_ctx* ctx) {
+  if (!ctx) return;
+  {
+    DeviceGuard g(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->in.release();
+    ctx->out.release();
+    ctx->out2.release();
+    ctx->meta.release();
+    (void)hipStreamDestroy(ctx->stream);
+  }
+  delete ctx;
+}
+
+void* sm_ctx_stream(sm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                   const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
+                                   const uint64_t* d_out_off, uint32_t* d_out_len, int mode, void* stream) {
+  if (!ctx || (mode != SM_MODE_REFERENCE && mode != SM_MODE_FAST)) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return SM_ERR_ARGUMENT;
+  DeviceGuard g(ctx->device);
+  sm::CompressArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nblk, 0, 1};
+  SM_CHECK(sm::launch_compress(a, mode, pick_stream(ctx, stream)));
+  return SM_OK;
+}
+
+sm_status sm_uncompress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                     const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
+                                     const uint64_t* d_out_off, const uint32_t* d_out_cap,
+                                     uint32_t* d_out_len, int32_t* d_status, void* stream) {
+  if (!ctx) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_cap || !d_out_len || !d_status)
+    return SM_ERR_ARGUMENT;
+  DeviceGuard g(ctx->device);
+  sm::DecompressArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_cap, d_out_len, d_status, nblk};
+  SM_CHECK(sm::launch_decompress(a, 0, pick_stream(ctx, stream)));
+  return SM_OK;
+}
+
+sm_status sm_compress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                            uint32_t nblk, uint8_t* out, const uint64_t* out_off, uint32_t* out_len, int mode) {
+  if (!ctx) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!in || !in_off || !in_len || !out || !out_off || !out_len) return SM_ERR_ARGUMENT;
+  size_t in_total = 0, out_total = 0;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    if (in_len[b] > SM_BLOCK_SIZE) return SM_ERR_ARGUMENT;
+    size_t ie = in_off[b] + in_len[b];
+    size_t oe = out_off[b] + sm_max_compressed_length(in_len[b]);
+    if (ie > in_total) in_total = ie;
+    if (oe > out_total) out_total = oe;
+  }
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  size_t meta_bytes = (size_t)nblk * (8 + 4 + 8 + 4);
+  SM_CHECK(ctx->in.ensure(in_total + 16));
+  SM_CHECK(ctx->out.ensure(out_total + 16));
+  SM_CHECK(ctx->meta.ensure(meta_bytes + 64));
+  uint8_t* m = (uint8_t*)ctx->meta.p;
+  uint64_t* d_in_off = (uint64_t*)m;
+  uint64_t* d_out_off = (uint64_t*)(m + 8 * (size_t)nblk);
+  uint32_t* d_in_len = (uint32_t*)(m + 16 * (size_t)nblk);
+  uint32_t* d_out_len = (uint32_t*)(m + 20 * (size_t)nblk);
+  SM_CHECK(hipMemcpyAsync(ctx->in.p, in, in_total, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_in_off, in_off, 8 * (size_t)nblk, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_out_off, out_off, 8 * (size_t)nblk, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_in_len, in_len, 4 * (size_t)nblk, hipMemcpyHostToDevice, s));
+  sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
+                     nblk, 0, 1};
+  SM_CHECK(sm::launch_compress(a, mode, s));
+  SM_CHECK(hipMemcpyAsync(out_len, d_out_len, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipStreamSynchronize(s));
+  // copy back only each block's bytes
+  for (uint32_t b = 0; b < nblk; ++b)
+    SM_CHECK(hipMemcpyAsync(out + out_off[b], (uint8_t*)ctx->out.p + out_off[b], out_len[b],
+                            hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipStreamSynchronize(s));
+  return SM_OK;
+}
+
+sm_status sm_uncompress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                              uint32_t nblk, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
+                              uint32_t* out_len, int32_t* status) {
+  if (!ctx) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len || !status) return SM_ERR_ARGUMENT;
+  size_t in_total = 0, out_total = 0;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    size_t ie = in_off[b] + in_len[b];
+    size_t oe = out_off[b] + out_cap[b];
+    if (ie > in_total) in_total = ie;
+    if (oe > out_total) out_total = oe;
+  }
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  size_t meta_bytes = (size_t)nblk * (8 + 8 + 4 + 4 + 4 + 4);
+  SM_CHECK(ctx->in.ensure(in_total + 16));
+  SM_CHECK(ctx->out.ensure(out_total + 16));
+  SM_CHECK(ctx->meta.ensure(meta_bytes + 64));
+  uint8_t* m = (uint8_t*)ctx->meta.p;
+  uint64_t* d_in_off = (uint64_t*)m;
+  uint64_t* d_out_off = (uint64_t*)(m + 8 * (size_t)nblk);
+  uint32_t* d_in_len = (uint32_t*)(m + 16 * (size_t)nblk);
+  uint32_t* d_out_cap = (uint32_t*)(m + 20 * (size_t)nblk);
+  uint32_t* d_out_len = (uint32_t*)(m + 24 * (size_t)nblk);
+  int32_t* d_status = (int32_t*)(m + 28 * (size_t)nblk);
+  SM_CHECK(hipMemcpyAsync(ctx->in.p, in, in_total, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_in_off, in_off, 8 * (size_t)nblk, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_out_off, out_off, 8 * (size_t)nblk, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_in_len, in_len, 4 * (size_t)nblk, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_out_cap, out_cap, 4 * (size_t)nblk, hipMemcpyHostToDevice, s));
+  sm::DecompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off,
+                       d_out_cap, d_out_len, d_status, nblk};
+  SM_CHECK(sm::launch_decompress(a, 0, s));
+  SM_CHECK(hipMemcpyAsync(out_len, d_out_len, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipMemcpyAsync(status, d_status, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipStreamSynchronize(s));
+  for (uint32_t b = 0; b < nblk; ++b)
+    if (status[b] == SM_OK && out_len[b])
+      SM_CHECK(hipMemcpyAsync(out + out_off[b], (uint8_t*)ctx->out.p + out_off[b], out_len[b],
+                              hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipStreamSynchronize(s));
+  return SM_OK;
+}
+
+// src/Snappy.jl:20-36 on the device: every 64 KiB fragment is one wave; fragments use the
+// table size of the WHOLE input (Q2) and no per-fragment header; a gather kernel then
+// concatenates them behind the varint header.
+sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed, size_t* compressed_length,
+                      int mode) {
+  if (!ctx || !compressed_length || (n && !input) || !compressed) return SM_ERR_ARGUMENT;
+  if (mode != SM_MODE_REFERENCE && mode != SM_MODE_FAST) return SM_ERR_ARGUMENT;
+  if (n > 0xffffffffull) return SM_ERR_INPUT_TOO_LARGE;                  // Snappy.jl:21
+  if (*compressed_length < sm_max_compressed_length(n)) return SM_BUFFER_TOO_SMALL;
+  uint8_t hdr[5];
+  size_t hl = sm_encode32(hdr, (uint32_t)n);                                // Snappy.jl:26
+  memcpy(compressed, hdr, hl);
+  if (n == 0) {
+    *compressed_length = hl;
+    return SM_OK;
+  }
+  const uint32_t nfrag = (uint32_t)((n + SM_BLOCK_SIZE - 1) / SM_BLOCK_SIZE);
+  const size_t slot = align_up(sm_max_compressed_length(SM_BLOCK_SIZE) + 8, 256);
+  std::vector<uint64_t> in_off(nfrag), out_off(nfrag), dst_off(nfrag);
+  std::vector<uint32_t> in_len(nfrag), out_len(nfrag);
+  for (uint32_t i = 0; i < nfrag; ++i) {
+    in_off[i] = (uint64_t)i * SM_BLOCK_SIZE;
+    size_t e = in_off[i] + SM_BLOCK_SIZE;
+    in_len[i] = (uint32_t)((e < n ? e : n) - in_off[i]);
+    out_off[i] = (uint64_t)i * slot;
+  }
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  SM_CHECK(ctx->in.ensure(n + 16));
+  SM_CHECK(ctx->out.ensure((size_t)nfrag * slot));
+  SM_CHECK(ctx->out2.ensure(sm_max_compressed_length(n) + 16));
+  SM_CHECK(ctx->meta.ensure((size_t)nfrag * 32 + 64));
+  uint8_t* m = (uint8_t*)ctx->meta.p;
+  uint64_t* d_in_off = (uint64_t*)m;
+  uint64_t* d_out_off = (uint64_t*)(m + 8 * (size_t)nfrag);
+  uint64_t* d_dst_off = (uint64_t*)(m + 16 * (size_t)nfrag);
+  uint32_t* d_in_len = (uint32_t*)(m + 24 * (size_t)nfrag);
+  uint32_t* d_out_len = (uint32_t*)(m + 28 * (size_t)nfrag);
+  SM_CHECK(hipMemcpyAsync(ctx->in.p, input, n, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_in_off, in_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_out_off, out_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_in_len, in_len.data(), 4 * (size_t)nfrag, hipMemcpyHostToDevice, s));
+  sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
+                     nfrag, sm::hashtable_size(n), 0};
+  SM_CHECK(sm::launch_compress(a, mode, s));
+  SM_CHECK(hipMemcpyAsync(out_len.data(), d_out_len, 4 * (size_t)nfrag, hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipStreamSynchronize(s));
+  size_t total = 0;
+  for (uint32_t i = 0; i < nfrag; ++i) {
+    dst_off[i] = total;
+    total += out_len[i];
+  }
+  if (hl + total > *compressed_length) return SM_BUFFER_TOO_SMALL;
+  SM_CHECK(hipMemcpyAsync(d_dst_off, dst_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
+  SM_CHECK(sm::launch_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_dst_off, (uint8_t*)ctx->out2.p,
+                             nfrag, s));
+  SM_CHECK(hipMemcpyAsync(compressed + hl, ctx->out2.p, total, hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipStreamSynchronize(s));
+  *compressed_length = hl + total;
+  return SM_OK;
+}
+
+// src/Snappy.jl:46-52: header parsed on the host (to size the output), the stream decoded by
+// one wave (foreign streams carry no fragment index).
+sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* uncompressed,
+                        size_t* uncompressed_length) {
+  if (!ctx || !uncompressed_length || (n && !compressed)) return SM_ERR_ARGUMENT;
+  uint32_t size = 0;
+  sm_status st = sm_parse32((const uint8_t*)compressed, n, 0, &size, nullptr);
+  if (st != SM_OK) return st;
+  if (n > 0xffffffffull) return SM_ERR_ARGUMENT;
+  if (*uncompressed_length < size) return SM_BUFFER_TOO_SMALL;
+  if (size && !uncompressed) return SM_ERR_ARGUMENT;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  SM_CHECK(ctx->in.ensure(n + 16));
+  SM_CHECK(ctx->out.ensure((size_t)size + 16));
+  SM_CHECK(ctx->meta.ensure(64));
+  uint8_t* m = (uint8_t*)ctx->meta.p;
+  uint64_t* d_off = (uint64_t*)m;           // in_off = out_off = 0
+  uint32_t* d_in_len = (uint32_t*)(m + 8);
+  uint32_t* d_cap = (uint32_t*)(m + 12);
+  uint32_t* d_out_len = (uint32_t*)(m + 16);
+  int32_t* d_status = (int32_t*)(m + 20);
+  uint32_t hv[2] = {(uint32_t)n, size};
+  uint64_t zero = 0;
+  SM_CHECK(hipMemcpyAsync(ctx->in.p, compressed, n, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_off, &zero, 8, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_in_len, hv, 8, hipMemcpyHostToDevice, s));
+  sm::DecompressArgs a{(const uint8_t*)ctx->in.p, d_off, d_in_len, (uint8_t*)ctx->out.p, d_off, d_cap, d_out_len,
+                       d_status, 1};
+  SM_CHECK(sm::launch_decompress(a, size > SM_BLOCK_SIZE, s));
+  int32_t dst = 0;
+  uint32_t dlen = 0;
+  SM_CHECK(hipMemcpyAsync(&dst, d_status, 4, hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipMemcpyAsync(&dlen, d_out_len, 4, hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipStreamSynchronize(s));
+  if (dst != SM_OK) return dst;
+  if (dlen) {
+    SM_CHECK(hipMemcpyAsync(uncompressed, ctx->out.p, dlen, hipMemcpyDeviceToHost, s));
+    SM_CHECK(hipStreamSynchronize(s));
+  }
+  *uncompressed_length = dlen;
+  return SM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,280 @@
+// sm_compress.hip -- batched 64 KiB-block snappy compression for gfx950 (MI355X).
+//
+// Two kernels, one wavefront (64 lanes) per block, block staged in LDS:
+//
+//  k_compress_exact  -- "reference mode": byte-identical to Snappy.jl's compress
+//                       (src/internal.jl:127-250 incl. quirks Q1/Q3, src/Snappy.jl:20-36 incl.
+//                       Q2).  The greedy parse is inherently serial (the u16 hash table at
+//                       internal.jl:189-193 carries state between probes), so it runs as
+//                       wave-uniform scalar code; the wave parallelises what is parallel:
+//                       block staging, table reset, find_match_length (256 B compared per
+//                       LDS round, internal.jl:343-387) and literal copies.
+//
+//  k_compress_fast   -- "fast mode": a wave-parallel LZ77 parse producing a valid snappy
+//                       stream (decodes bit-exactly under Snappy.jl's uncompress) but not the
+//                       reference's bytes.  256 positions per step (4 per lane): every
+//                       position is hashed, candidates come from a u32 latest-position table
+//                       (ds_max_u32, deterministic), are verified and extended in parallel,
+//                       then a scalar greedy walk over the match ballot picks copies.
+//
+// Data layout in HBM: input blocks at in[in_off[b]], outputs at out[out_off[b]] (caller
+// reserves max_compressed_length(len)+5 per block, i.e. fixed slots), out_len[b] = bytes.
+#include "sm_device.h"
+#include "sm_internal.h"
+
+namespace sm {
+
+constexpr uint32_t kLdsPad = 64;  // readable slack after the block for lds_ld32 / wave compares
+
+// ---- output emission (global memory, wave-uniform op) -------------------------------
+
+__device__ inline uint32_t emit_varint(uint8_t* dst, uint32_t op, uint32_t v, uint32_t lane) {
+  uint32_t nb = varint_len(v);
+  if (lane < nb) dst[op + lane] = (uint8_t)(((v >> (7 * lane)) & 0x7f) | (lane + 1 < nb ? 0x80 : 0));
+  return op + nb;
+}
+
+// internal.jl:252-287.  ref_q3: one-byte tag only for len < 60 (Snappy.jl); else len-1 < 60.
+__device__ inline uint32_t emit_literal_g(uint8_t* dst, uint32_t op, const uint8_t* lds, uint32_t start,
+                                          uint32_t len, uint32_t lane, bool ref_q3) {
+  uint32_t n = len - 1;
+  bool one = ref_q3 ? (len < 60) : (n < 60);
+  if (one) {
+    if (lane == 0) dst[op] = (uint8_t)(n << 2);
+    op += 1;
+  } else {
+    uint32_t count = n < 256 ? 1 : n < 65536 ? 2 : n < (1u << 24) ? 3 : 4;
+    if (lane == 0) dst[op] = (uint8_t)((59 + count) << 2);
+    if (lane >= 1 && lane <= count) dst[op + lane] = (uint8_t)(n >> (8 * (lane - 1)));
+    op += 1 + count;
+  }
+  wave_copy_lds_to_global(dst + op, lds, start, len, lane);
+  return op + len;
+}
+
+// internal.jl:289-304 (single lane)
+__device__ inline uint32_t put_copy_upto_64(uint8_t* dst, uint32_t op, uint32_t offset, uint32_t len) {
+  if (len < 12 && offset < 2048) {
+    dst[op] = (uint8_t)(1 + ((len - 4) << 2) + ((offset >> 3) & 0xe0));
+    dst[op + 1] = (uint8_t)offset;
+    return op + 2;
+  }
+  dst[op] = (uint8_t)(2 + ((len - 1) << 2));
+  dst[op + 1] = (uint8_t)offset;
+  dst[op + 2] = (uint8_t)(offset >> 8);
+  return op + 3;
+}
+
+// internal.jl:306-329 (single lane)
+__device__ inline uint32_t put_copy(uint8_t* dst, uint32_t op, uint32_t offset, uint32_t len) {
+  if (len < 12) return put_copy_upto_64(dst, op, offset, len);
+  while (len >= 68) { op = put_copy_upto_64(dst, op, offset, 64); len -= 64; }
+  if (len > 64) { op = put_copy_upto_64(dst, op, offset, 60); len -= 60; }
+  return put_copy_upto_64(dst, op, offset, len);
+}
+
+__device__ inline uint32_t emit_copy_g(uint8_t* dst, uint32_t op, uint32_t offset, uint32_t len, uint32_t lane) {
+  if (lane == 0) put_copy(dst, op, offset, len);
+  return op + copy_tag_bytes(offset, len);
+}
+
+__device__ inline uint32_t uld32(const uint8_t* lds, uint32_t pos) { return uniform(lds_ld32(lds, pos)); }
+
+// ---- reference mode ------------------------------------------------------------------
+
+__global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t sdata[kBlockSize + kLdsPad];
+  __shared__ __attribute__((aligned(16))) uint16_t stab[kMaxHashTableSize];
+
+  const uint32_t b = blockIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t n = a.in_len[b];
+  const uint8_t* src = a.in + a.in_off[b];
+  uint8_t* dst = a.out + a.out_off[b];
+  if (n > kBlockSize) {  // batch contract violated: refuse instead of overrunning LDS
+    if (lane == 0) a.out_len[b] = 0xffffffffu;
+    return;
+  }
+
+  wave_load_global_to_lds(sdata, src, n, lane);
+  if (lane < kLdsPad) sdata[n + lane] = 0;
+  const uint32_t tsize = a.table_size ? a.table_size : hashtable_size(n);      // Snappy.jl:27 (Q2)
+  const uint32_t shift = 32 - (31 - __builtin_clz(tsize));                     // internal.jl:128
+  {
+    uint32_t* t32 = reinterpret_cast<uint32_t*>(stab);
+    for (uint32_t k = lane; k < tsize / 2; k += kWave) t32[k] = 0xffffffffu;   // Snappy.jl:30
+  }
+  __syncthreads();
+
+  uint32_t op = a.header ? emit_varint(dst, 0, n, lane) : 0;                   // Snappy.jl:26
+  if (n == 0) {
+    if (lane == 0) a.out_len[b] = op;
+    return;
+  }
+  const uint32_t e = n - 1;                  // inclusive end (ip_end)
+  const int32_t ip_limit = (int32_t)n - 16;  // internal.jl:131, Q1: 1-based ip_end-15
+  uint32_t ip = 0, next_emit = 0, cand = 0;
+
+  if (n >= kInputMarginBytes) {                                                // internal.jl:133
+    for (;;) {
+      uint32_t skip = 32;                                                      // :162
+      ip += 1;                                                                 // :163
+      uint32_t next_hash = hash32(uld32(sdata, ip), shift);
+      uint32_t next_ip = ip;
+      for (;;) {                                                               // :167-194
+        ip = next_ip;
+        uint32_t cur_hash = next_hash;
+        uint32_t step = skip >> 5;
+        skip += step;
+        next_ip = ip + step;
+        if ((int32_t)next_ip > ip_limit) goto emit_remainder;                  // :175
+        next_hash = hash32(uld32(sdata, next_ip), shift);
+        cand = (uint16_t)(uniform(stab[cur_hash]) + 1);                        // :190
+        if (lane == 0) stab[cur_hash] = (uint16_t)(ip - 1);                    // :191
+        if (uld32(sdata, cand) == uld32(sdata, ip)) break;                     // :193
+      }
+      op = emit_literal_g(dst, op, sdata, next_emit, ip - next_emit, lane, true);   // :200
+      for (;;) {                                                               // :211-239
+        uint32_t avail = e - (ip + 4) + 1;
+        uint32_t matched = 4 + wave_match_length(sdata, cand + 4, ip + 4, avail, lane);  // :216
+        op = emit_copy_g(dst, op, ip - cand, matched, lane);                   // :217
+        ip += matched;
+        next_emit = ip;
+        if ((int32_t)ip >= ip_limit) goto emit_remainder;                      // :222
+        uint32_t prev_hash = hash32(uld32(sdata, ip - 1), shift);              // :228
+        uint32_t input_bytes = uld32(sdata, ip);
+        uint32_t cur_hash = hash32(input_bytes, shift);
+        if (lane == 0) stab[prev_hash] = (uint16_t)(ip - 2);                   // :233
+        cand = (uint16_t)(uniform(stab[cur_hash]) + 1);                        // :234
+        if (lane == 0) stab[cur_hash] = (uint16_t)(ip - 1);                    // :235
+        if (input_bytes != uld32(sdata, cand)) break;                          // :238
+      }
+    }
+  }
+emit_remainder:
+  if (next_emit <= e) op = emit_literal_g(dst, op, sdata, next_emit, e - next_emit + 1, lane, true);  // :244-248
+  if (lane == 0) a.out_len[b] = op;
+}
+
+// ---- fast mode -----------------------------------------------------------------------
+
+constexpr uint32_t kFastHashBits = 12;                  // 4096-entry table
+constexpr uint32_t kFastTable = 1u << kFastHashBits;
+constexpr uint32_t kFastShift = 32 - kFastHashBits;
+constexpr uint32_t kFastExtCap = 12;                    // eager per-lane extension (bytes past the first 4)
+
+__global__ __launch_bounds__(64) void k_compress_fast(CompressArgs a) {
+  // 80 KiB exactly, so two blocks fit a CU's 160 KiB.  No pad: over-reads past the block
+  // land in the table and are always masked by the length caps (results never depend on them).
+  __shared__ __attribute__((aligned(16))) uint8_t smem[kBlockSize + 4 * kFastTable];
+  uint8_t* sdata = smem;
+  uint32_t* stab = reinterpret_cast<uint32_t*>(smem + kBlockSize);   // latest position + 1 (0 = empty)
+
+  const uint32_t b = blockIdx.x;
+  const uint32_t lane = lane_id();
+  const uint32_t n = a.in_len[b];
+  const uint8_t* src = a.in + a.in_off[b];
+  uint8_t* dst = a.out + a.out_off[b];
+  if (n > kBlockSize) {  // batch contract violated: refuse instead of overrunning LDS
+    if (lane == 0) a.out_len[b] = 0xffffffffu;
+    return;
+  }
+
+  wave_load_global_to_lds(sdata, src, n, lane);
+  for (uint32_t k = lane; k < kFastTable; k += kWave) stab[k] = 0;
+  __syncthreads();
+
+  uint32_t op = a.header ? emit_varint(dst, 0, n, lane) : 0;
+  uint32_t lit_start = 0;  // first byte not yet emitted
+  uint32_t p = 0;          // parse position (next byte not covered by a chosen copy)
+  const uint32_t qend = n >= 4 ? n - 3 : 0;   // match starts q < qend (q + 4 <= n)
+
+  for (uint32_t c0 = 0; c0 < qend; c0 += 4 * kWave) {
+    if (p >= c0 + 4 * kWave) continue;  // whole step covered by an earlier copy
+    uint32_t cand[4], ml[4];
+    uint64_t mm[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t q = c0 + 64 * j + lane;
+      bool valid = q < qend;
+      uint32_t w = lds_ld32(sdata, q);
+      uint32_t h = hash32(w, kFastShift);
+      uint32_t t = valid ? stab[h] : 0;     // sees every position of earlier sub-steps
+      if (valid) atomicMax(&stab[h], q + 1);
+      bool ok = valid && t != 0;
+      uint32_t c = t - 1;
+      ok = ok && c < q && lds_ld32(sdata, c) == w;
+      uint32_t len = 0;
+      if (ok) {
+        uint32_t avail = n - q - 4;
+        uint32_t cap = avail < kFastExtCap ? avail : kFastExtCap;
+        uint32_t ext = 0;
+        while (ext < cap) {
+          uint32_t x = lds_ld32(sdata, c + 4 + ext) ^ lds_ld32(sdata, q + 4 + ext);
+          if (x) { ext += __builtin_ctz(x) >> 3; break; }
+          ext += 4;
+        }
+        if (ext > cap) ext = cap;
+        len = 4 + ext;
+      }
+      cand[j] = c;
+      ml[j] = len;
+      mm[j] = ballot(ok);
+    }
+    // scalar greedy walk over the match masks
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t s0 = c0 + 64 * j;
+      for (;;) {
+        if (p >= s0 + 64) break;
+        uint32_t rel = p > s0 ? p - s0 : 0;
+        uint64_t m = rel >= 64 ? 0 : (mm[j] >> rel);
+        if (!m) break;
+        uint32_t l = rel + ctz64(m);
+        uint32_t q = s0 + l;
+        uint32_t L = readlane(ml[j], l);
+        uint32_t c = readlane(cand[j], l);
+        if (L == 4 + kFastExtCap && q + L < n) {
+          // capped: finish the extension cooperatively
+          L += wave_match_length(sdata, c + L, q + L, n - q - L, lane);
+        }
+        if (q > lit_start) op = emit_literal_g(dst, op, sdata, lit_start, q - lit_start, lane, false);
+        op = emit_copy_g(dst, op, q - c, L, lane);
+        p = q + L;
+        lit_start = p;
+      }
+    }
+  }
+  if (lit_start < n) op = emit_literal_g(dst, op, sdata, lit_start, n - lit_start, lane, false);
+  if (lane == 0) a.out_len[b] = op;
+}
+
+// ---- gather (single-stream assembly) ---------------------------------------------------
+
+__global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ src, const uint64_t* src_off,
+                                                 const uint32_t* len, const uint64_t* dst_off,
+                                                 uint8_t* __restrict__ dst) {
+  const uint32_t b = blockIdx.x;
+  const uint8_t* s = src + src_off[b];
+  uint8_t* d = dst + dst_off[b];
+  const uint32_t n = len[b];
+  for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) d[k] = s[k];
+}
+
+hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s) {
+  if (a.nblk == 0) return hipSuccess;
+  if (mode == 0)
+    hipLaunchKernelGGL(k_compress_exact, dim3(a.nblk), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_compress_fast, dim3(a.nblk), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
+                         const uint64_t* dst_off, uint8_t* dst, uint32_t nblk, hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather, dim3(nblk), dim3(256), 0, s, src, src_off, len, dst_off, dst);
+  return hipGetLastError();
+}
+
+}  // namespace sm

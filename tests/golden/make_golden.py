@@ -47,8 +47,26 @@ EDGE_STRINGS = [
 ]
 
 
+REFERENCE_INTERNAL = "/root/reference/src/internal.jl"
+
+
+def char_table_from_reference():
+    """CHAR_TABLE values (src/internal.jl:47-80) as data, for the derived-table check."""
+    import re
+    src = open(REFERENCE_INTERNAL).read()
+    body = src[src.index("CHAR_TABLE = UInt16["):]
+    body = body[: body.index("]")]
+    vals = [int(v, 16) for v in re.findall(r"0x[0-9a-fA-F]{4}", body)]
+    assert len(vals) == 256
+    return vals
+
+
 def main():
     out = {"corpus": {}, "edge_strings": []}
+    if os.path.exists(REFERENCE_INTERNAL):
+        out["char_table"] = char_table_from_reference()
+    else:
+        out["char_table"] = json.load(open(os.path.join(HERE, "golden.json")))["char_table"]
     for f in sorted(SURVEY_TABLE):
         raw = open(os.path.join(HERE, "testdata", f), "rb").read()
         ref = O.compress(raw)

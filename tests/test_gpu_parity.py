@@ -1,0 +1,206 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle on the same inputs.
+
+* reference mode: compressed bytes identical to the oracle (= Snappy.jl) -- whole-buffer API
+  (multi-fragment streams, quirk Q2) and batched 64 KiB blocks;
+* fast mode: every stream decodes bit-exactly under the oracle decoder and libsnappy;
+* decompress: output and status code identical to the oracle, incl. corrupted streams and
+  a seeded mutation fuzz (first error in stream order, F6 leniencies).
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, ROUNDTRIP_FILES, read_testfile
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+
+
+def blocks_of(data, size=65536):
+    return [data[i:i + size] for i in range(0, len(data), size)] or [b""]
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    return {f: read_testfile(f) for f in sorted(GOLDEN["corpus"])}
+
+
+# ---- reference mode -------------------------------------------------------------------
+
+@pytest.mark.parametrize("fname", sorted(GOLDEN["corpus"]))
+def test_reference_mode_whole_file_matches_golden(sm, gpu_available, fname):
+    raw = read_testfile(fname)
+    out = sm.compress(raw)                      # Snappy.jl compress(), multi-fragment, Q2 table
+    g = GOLDEN["corpus"][fname]
+    assert len(out) == g["c_reference"]
+    assert hashlib.sha256(out).hexdigest() == g["sha256_reference"]
+
+
+def test_reference_mode_batched_blocks(sm, oracle, gpu_available, corpus):
+    blocks = []
+    for raw in corpus.values():
+        blocks.extend(blocks_of(raw))
+    outs = sm.compress_batch(blocks, mode="reference")
+    for blk, out in zip(blocks, outs):
+        assert out == oracle.compress(blk)
+
+
+def test_reference_mode_edge_strings(sm, oracle, gpu_available):
+    from golden.make_golden import EDGE_STRINGS
+    for s, g in zip(EDGE_STRINGS, GOLDEN["edge_strings"]):
+        out = sm.compress(s)
+        assert hashlib.sha256(out).hexdigest() == g["sha256_reference"]
+        assert sm.uncompress(out) == s
+    assert sm.compress("abc") == bytes.fromhex("0308616263")      # String method, Snappy.jl:38
+
+
+def test_reference_mode_small_sizes(sm, oracle, gpu_available):
+    rng = np.random.default_rng(11)
+    blocks = []
+    for n in list(range(0, 80)) + [255, 256, 257, 4095, 4096, 16383, 16384, 16385, 65535, 65536]:
+        kind = n % 3
+        if kind == 0:
+            blk = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 1:
+            blk = (b"abcab" * (n // 5 + 1))[:n]
+        else:
+            blk = rng.integers(0, 4, n, dtype=np.uint8).tobytes()
+        blocks.append(blk)
+    outs = sm.compress_batch(blocks, mode="reference")
+    for blk, out in zip(blocks, outs):
+        assert out == oracle.compress(blk), len(blk)
+
+
+def test_reference_mode_dictionary_streams(sm, oracle, gpu_available):
+    from test_oracle import dictionary_stream
+    rng = np.random.default_rng(0x5EED)
+    for _ in range(6):
+        raw = dictionary_stream(rng, 1 << 14)
+        assert sm.compress(raw) == oracle.compress(raw)
+
+
+# ---- fast mode --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("fname", ROUNDTRIP_FILES)
+def test_fast_mode_roundtrip_whole_file(sm, oracle, libsnappy, gpu_available, fname):
+    raw = read_testfile(fname)
+    out = sm.compress(raw, mode="fast")
+    assert oracle.uncompress(out) == raw
+    assert libsnappy.uncompress(out) == raw
+    assert sm.uncompress(out) == raw
+
+
+def test_fast_mode_batched_roundtrip(sm, oracle, libsnappy, gpu_available, corpus):
+    rng = np.random.default_rng(5)
+    blocks = []
+    for raw in corpus.values():
+        blocks.extend(blocks_of(raw))
+    for n in list(range(0, 70)) + [65535, 65536]:
+        blocks.append(rng.integers(0, 3, n, dtype=np.uint8).tobytes())
+    blocks.append(b"\x00" * 65536)
+    blocks.append(rng.integers(0, 256, 65536, dtype=np.uint8).tobytes())
+    outs = sm.compress_batch(blocks, mode="fast")
+    for blk, out in zip(blocks, outs):
+        assert oracle.uncompress(out) == blk
+        assert libsnappy.uncompress(out) == blk
+    ratio = sum(map(len, outs)) / sum(map(len, blocks))
+    ref = sum(len(oracle.compress(b)) for b in blocks) / sum(map(len, blocks))
+    assert ratio < ref * 1.10, (ratio, ref)   # fast parse stays within 10% of the reference size
+
+
+# ---- decompress -------------------------------------------------------------------------
+
+def test_decompress_corpus_and_golden(sm, oracle, libsnappy, gpu_available, corpus):
+    streams = [oracle.compress(raw) for raw in corpus.values()]
+    streams.append(read_testfile("alice29.snappy"))
+    for s in streams:
+        assert sm.uncompress(s) == oracle.uncompress(s)
+
+
+def test_decompress_batched_blocks(sm, oracle, gpu_available, corpus):
+    streams = []
+    for raw in corpus.values():
+        streams.extend(oracle.compress(b) for b in blocks_of(raw))
+    outs, status = sm.uncompress_batch(streams)
+    assert not status.any()
+    for s, o in zip(streams, outs):
+        assert o == oracle.uncompress(s)
+
+
+def _status(sm, data):
+    try:
+        return 0, sm.uncompress(data)
+    except sm.SnappyError as e:
+        return e.code, None
+
+
+def test_decompress_corrupted_matches_oracle(sm, oracle, gpu_available):
+    from test_oracle import corrupted_cases
+    for c in corrupted_cases(oracle):
+        st_o, out_o = oracle.uncompress_status(c)
+        st_g, out_g = _status(sm, c)
+        assert st_o != 0
+        assert (st_g, out_g) == (st_o, out_o)
+
+
+def test_decompress_leniencies(sm, gpu_available, oracle):
+    good = oracle.compress(b"hello hello hello hello")
+    assert sm.uncompress(good + b"\x07") == b"hello hello hello hello"
+    assert sm.uncompress(b"\x00\x00") == b""
+    assert sm.uncompress(b"\x00") == b""
+    assert _status(sm, b"\x00\x00\x00")[0] == 21
+    assert _status(sm, bytes([0x40, 0x12, 0x00, 0x00]))[0] == 19
+
+
+def test_decompress_mutation_fuzz_batched(sm, oracle, gpu_available):
+    """Seeded byte flips / truncations / extensions of valid streams: identical status codes
+    (first error in stream order) and outputs vs the oracle, decoded as one GPU batch."""
+    rng = np.random.default_rng(1234)
+    base = [oracle.compress(read_testfile(f)[:4096]) for f in ("html", "alice29.txt", "kppkn.gtb", "urls.10K")]
+    base += [oracle.compress(b"ab" * 700), oracle.compress(bytes(range(256)) * 3)]
+    cases = []
+    for i in range(3000):
+        s = bytearray(base[i % len(base)])
+        kind = rng.integers(0, 4)
+        if kind == 0:
+            for _ in range(int(rng.integers(1, 4))):
+                s[int(rng.integers(0, len(s)))] = int(rng.integers(0, 256))
+        elif kind == 1:
+            s = s[: int(rng.integers(0, len(s)))]
+        elif kind == 2:
+            s += rng.integers(0, 256, int(rng.integers(1, 6)), dtype=np.uint8).tobytes()
+        else:
+            p = int(rng.integers(1, len(s)))
+            s[p] = int(rng.integers(0, 256))
+            s = s[: max(1, len(s) - int(rng.integers(0, 8)))]
+        cases.append(bytes(s))
+    caps = []
+    for c in cases:
+        try:
+            caps.append(min(oracle.uncompressed_length(c), 1 << 20))
+        except oracle.OracleError:
+            caps.append(0)
+    outs, status = sm.uncompress_batch(cases, capacities=caps)
+    for c, cap, o, st in zip(cases, caps, outs, status):
+        try:
+            n = oracle.uncompressed_length(c)
+        except oracle.OracleError as e:
+            assert st == e.code
+            continue
+        if n > cap:
+            assert st == 2
+            continue
+        st_o, out_o = oracle.uncompress_status(c)
+        assert int(st) == st_o
+        assert o == out_o
+
+
+def test_decompress_large_stream_global_path(sm, oracle, gpu_available):
+    # > 64 KiB declared length: decoded straight into HBM (single stream)
+    raw = read_testfile("html_x_4") + read_testfile("urls.10K")[:100000]
+    comp = oracle.compress(raw)
+    assert sm.uncompress(comp) == raw
