@@ -86,7 +86,8 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t compressed_l
  * an independent snappy stream (varint header + one compress_fragment!, i.e. exactly
  * compress(block) of src/Snappy.jl:20-36) written at d_out + d_out_off[b], which must have
  * room for sm_max_compressed_length(d_in_len[b]) bytes.  d_out_len[b] receives its size
- * (0xffffffff if the block was longer than 64 KiB).  stream: hipStream_t or NULL = ctx stream. */
+ * (0xffffffff if the block was longer than 64 KiB).  stream: the hipStream_t to launch on
+ * (NULL = the default stream, as everywhere in HIP); nothing is synchronised. */
 sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
                                    const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                    const uint64_t* d_out_off, uint32_t* d_out_len, int mode, void* stream);

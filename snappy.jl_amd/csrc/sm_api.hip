@@ -56,7 +56,6 @@ struct DeviceGuard {
   }
 };
 
-inline hipStream_t pick_stream(sm_ctx* ctx, void* s) { return s ? (hipStream_t)s : ctx->stream; }
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
@@ -169,7 +168,7 @@ sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint6
   if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return SM_ERR_ARGUMENT;
   DeviceGuard g(ctx->device);
   sm::CompressArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nblk, 0, 1};
-  SM_CHECK(sm::launch_compress(a, mode, pick_stream(ctx, stream)));
+  SM_CHECK(sm::launch_compress(a, mode, (hipStream_t)stream));
   return SM_OK;
 }
 
@@ -183,7 +182,7 @@ sm_status sm_uncompress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uin
     return SM_ERR_ARGUMENT;
   DeviceGuard g(ctx->device);
   sm::DecompressArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_cap, d_out_len, d_status, nblk};
-  SM_CHECK(sm::launch_decompress(a, 0, pick_stream(ctx, stream)));
+  SM_CHECK(sm::launch_decompress(a, 0, (hipStream_t)stream));
   return SM_OK;
 }
 

@@ -10,12 +10,7 @@
 //                       block staging, table reset, find_match_length (256 B compared per
 //                       LDS round, internal.jl:343-387) and literal copies.
 //
-//  k_compress_fast   -- "fast mode": a wave-parallel LZ77 parse producing a valid snappy
-//                       stream (decodes bit-exactly under Snappy.jl's uncompress) but not the
-//                       reference's bytes.  256 positions per step (4 per lane): every
-//                       position is hashed, candidates come from a u32 latest-position table
-//                       (ds_max_u32, deterministic), are verified and extended in parallel,
-//                       then a scalar greedy walk over the match ballot picks copies.
+//  k_compress_fast   -- "fast mode", see sm_compress_fast.hip.
 //
 // Data layout in HBM: input blocks at in[in_off[b]], outputs at out[out_off[b]] (caller
 // reserves max_compressed_length(len)+5 per block, i.e. fixed slots), out_len[b] = bytes.
@@ -156,99 +151,6 @@ emit_remainder:
   if (lane == 0) a.out_len[b] = op;
 }
 
-// ---- fast mode -----------------------------------------------------------------------
-
-constexpr uint32_t kFastHashBits = 12;                  // 4096-entry table
-constexpr uint32_t kFastTable = 1u << kFastHashBits;
-constexpr uint32_t kFastShift = 32 - kFastHashBits;
-constexpr uint32_t kFastExtCap = 12;                    // eager per-lane extension (bytes past the first 4)
-
-__global__ __launch_bounds__(64) void k_compress_fast(CompressArgs a) {
-  // 80 KiB exactly, so two blocks fit a CU's 160 KiB.  No pad: over-reads past the block
-  // land in the table and are always masked by the length caps (results never depend on them).
-  __shared__ __attribute__((aligned(16))) uint8_t smem[kBlockSize + 4 * kFastTable];
-  uint8_t* sdata = smem;
-  uint32_t* stab = reinterpret_cast<uint32_t*>(smem + kBlockSize);   // latest position + 1 (0 = empty)
-
-  const uint32_t b = blockIdx.x;
-  const uint32_t lane = lane_id();
-  const uint32_t n = a.in_len[b];
-  const uint8_t* src = a.in + a.in_off[b];
-  uint8_t* dst = a.out + a.out_off[b];
-  if (n > kBlockSize) {  // batch contract violated: refuse instead of overrunning LDS
-    if (lane == 0) a.out_len[b] = 0xffffffffu;
-    return;
-  }
-
-  wave_load_global_to_lds(sdata, src, n, lane);
-  for (uint32_t k = lane; k < kFastTable; k += kWave) stab[k] = 0;
-  __syncthreads();
-
-  uint32_t op = a.header ? emit_varint(dst, 0, n, lane) : 0;
-  uint32_t lit_start = 0;  // first byte not yet emitted
-  uint32_t p = 0;          // parse position (next byte not covered by a chosen copy)
-  const uint32_t qend = n >= 4 ? n - 3 : 0;   // match starts q < qend (q + 4 <= n)
-
-  for (uint32_t c0 = 0; c0 < qend; c0 += 4 * kWave) {
-    if (p >= c0 + 4 * kWave) continue;  // whole step covered by an earlier copy
-    uint32_t cand[4], ml[4];
-    uint64_t mm[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint32_t q = c0 + 64 * j + lane;
-      bool valid = q < qend;
-      uint32_t w = lds_ld32(sdata, q);
-      uint32_t h = hash32(w, kFastShift);
-      uint32_t t = valid ? stab[h] : 0;     // sees every position of earlier sub-steps
-      if (valid) atomicMax(&stab[h], q + 1);
-      bool ok = valid && t != 0;
-      uint32_t c = t - 1;
-      ok = ok && c < q && lds_ld32(sdata, c) == w;
-      uint32_t len = 0;
-      if (ok) {
-        uint32_t avail = n - q - 4;
-        uint32_t cap = avail < kFastExtCap ? avail : kFastExtCap;
-        uint32_t ext = 0;
-        while (ext < cap) {
-          uint32_t x = lds_ld32(sdata, c + 4 + ext) ^ lds_ld32(sdata, q + 4 + ext);
-          if (x) { ext += __builtin_ctz(x) >> 3; break; }
-          ext += 4;
-        }
-        if (ext > cap) ext = cap;
-        len = 4 + ext;
-      }
-      cand[j] = c;
-      ml[j] = len;
-      mm[j] = ballot(ok);
-    }
-    // scalar greedy walk over the match masks
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t s0 = c0 + 64 * j;
-      for (;;) {
-        if (p >= s0 + 64) break;
-        uint32_t rel = p > s0 ? p - s0 : 0;
-        uint64_t m = rel >= 64 ? 0 : (mm[j] >> rel);
-        if (!m) break;
-        uint32_t l = rel + ctz64(m);
-        uint32_t q = s0 + l;
-        uint32_t L = readlane(ml[j], l);
-        uint32_t c = readlane(cand[j], l);
-        if (L == 4 + kFastExtCap && q + L < n) {
-          // capped: finish the extension cooperatively
-          L += wave_match_length(sdata, c + L, q + L, n - q - L, lane);
-        }
-        if (q > lit_start) op = emit_literal_g(dst, op, sdata, lit_start, q - lit_start, lane, false);
-        op = emit_copy_g(dst, op, q - c, L, lane);
-        p = q + L;
-        lit_start = p;
-      }
-    }
-  }
-  if (lit_start < n) op = emit_literal_g(dst, op, sdata, lit_start, n - lit_start, lane, false);
-  if (lane == 0) a.out_len[b] = op;
-}
-
 // ---- gather (single-stream assembly) ---------------------------------------------------
 
 __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ src, const uint64_t* src_off,
@@ -263,10 +165,8 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ src,
 
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s) {
   if (a.nblk == 0) return hipSuccess;
-  if (mode == 0)
-    hipLaunchKernelGGL(k_compress_exact, dim3(a.nblk), dim3(64), 0, s, a);
-  else
-    hipLaunchKernelGGL(k_compress_fast, dim3(a.nblk), dim3(64), 0, s, a);
+  if (mode != 0) return launch_compress_fast(a, s);
+  hipLaunchKernelGGL(k_compress_exact, dim3(a.nblk), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -34,6 +34,7 @@ struct DecompressArgs {
 
 // mode 0 = reference (byte-identical to Snappy.jl), 1 = fast (wave-parallel parse)
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s);
+hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s);
 hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)
 hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
