@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) void k_compress_fast(CompressArgs a) {
 
   const uint32_t b = blockIdx.x;
   const uint32_t tid = threadIdx.x;
-  const uint32_t wave = tid >> 6;
+  const uint32_t wave = uniform(tid >> 6);  // readfirstlane: lets the walk compile to SALU
   const uint32_t lane = tid & 63;
   const uint32_t n = a.in_len[b];
   const uint8_t* src = a.in + a.in_off[b];

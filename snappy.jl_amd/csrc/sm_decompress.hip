@@ -9,37 +9,53 @@
 //   * the copy-length check is skipped on the 2x8-byte fast path (internal.jl:500-505).
 // The first error in stream order wins, as the reference throws at the first one.
 //
-// Tag walk: the wave keeps a 256-byte window of the compressed stream in VGPRs (4 B/lane)
-// and reads tag bytes with v_readlane (wave-uniform scalar walk).  Each tag's bytes are then
-// moved wave-wide: literals global->output, copies output->output with RLE handled as
-// src = op - offset + (k mod offset), which is the byte the reference's sequential
-// incremental_copy_slow! (internal.jl:477-481) would read.
-// Output: staged in LDS when the declared length is <= 64 KiB (every block the compressor
-// produces), then written with 16-B stores; longer streams decode straight into HBM.
+// Batched tag engine (declared length <= 64 KiB -- every block the compressor produces):
+//  * output written straight to HBM (the block's output region), so a wave needs only its
+//    1 KiB LDS ring and occupancy is set by VGPRs (many blocks in flight per CU hide the
+//    store->load latency of copies); a workgroup-scope fence (s_waitcnt) orders a round's
+//    copy-source loads after the earlier rounds' stores of the same wave;
+//  * the compressed stream flows through a 1 KiB LDS ring (4 x 256-B slots + 16-B mirror),
+//    one slot prefetched into registers a batch ahead;
+//  * every lane computes, for its 4 positions of the current slot, the size a tag starting
+//    there would have (packed u8, 255 = literal too long for a batch), so the serial tag walk
+//    is one v_readlane + a few SALU ops per tag;
+//  * up to 64 tags per batch decode one per lane (unaligned ds_read_b64 of the ring), output
+//    offsets from a wave scan, the reference's error checks per tag -- the lowest failing lane
+//    decides the status;
+//  * tags execute lane-parallel in 8-byte chunks (unaligned global dwordx2 loads/stores), in
+//    dependency rounds: a copy runs once every earlier tag of the batch its source overlaps
+//    has run.  Overlapping copies (offset < 8) first build the 8-byte period pattern, then
+//    advance with an effective offset that is a multiple of the period -- exactly the bytes
+//    incremental_copy_slow! (internal.jl:477-481) produces.
+// Literals longer than 64 bytes are copied by the whole wave.
+// Streams declaring > 64 KiB use a simple per-tag engine (also straight into HBM).
 #include "sm_device.h"
 #include "sm_internal.h"
 
 namespace sm {
 
-struct Window {
-  uint32_t w;      // 4 bytes per lane, little-endian
-  uint32_t base;   // stream position of lane 0 byte 0
-};
+typedef uint16_t __attribute__((aligned(1))) du16u;
+typedef uint32_t __attribute__((aligned(1))) du32u;
+typedef uint64_t __attribute__((aligned(1))) du64u;
 
-__device__ inline void win_load(Window& win, const uint8_t* __restrict__ in, uint32_t N, uint32_t pos, uint32_t lane) {
-  uint32_t p = pos + 4 * lane;
+constexpr uint32_t kRing = 1024;
+
+__device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
+  if (p + 3 < N && (((uintptr_t)(in + p)) & 3) == 0) return *reinterpret_cast<const uint32_t*>(in + p);
   uint32_t v = 0;
-  if (p + 3 < N && (((uintptr_t)(in + p)) & 3) == 0) {
-    v = *reinterpret_cast<const uint32_t*>(in + p);
-  } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) v |= (p + k < N ? (uint32_t)in[p + k] : 0u) << (8 * k);
-  }
-  win.w = v;
-  win.base = pos;
+  for (int k = 0; k < 4; ++k) v |= (p + k < N ? (uint32_t)in[p + k] : 0u) << (8 * k);
+  return v;
 }
 
-// 4 bytes at stream position pos (zero past N), window must cover pos..pos+7
+// ---------------------------------------------------------------------------------------
+// simple per-tag engine (streams declaring > 64 KiB, output in HBM)
+
+struct Window {
+  uint32_t w;
+  uint32_t base;
+};
+
 __device__ inline uint32_t win_ld32(const Window& win, uint32_t pos) {
   uint32_t rel = pos - win.base;
   uint32_t lo = readlane(win.w, rel >> 2);
@@ -47,50 +63,44 @@ __device__ inline uint32_t win_ld32(const Window& win, uint32_t pos) {
   return __builtin_amdgcn_alignbyte(hi, lo, rel & 3);
 }
 
-template <bool kLds>
-__device__ inline int32_t decode_stream(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t size,
+__device__ int32_t decode_stream_global(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t size,
                                         uint8_t* out, uint32_t lane) {
   Window win;
-  win_load(win, in, N, ip, lane);
+  win.w = load_word(in, N, ip + 4 * lane);
+  win.base = ip;
   uint32_t op = 0;
+  volatile uint8_t* vo = out;
   while ((int64_t)ip < (int64_t)N - 1) {                                 // internal.jl:416
-    if (ip - win.base > 4 * kWave - 8) win_load(win, in, N, ip, lane);
+    if (ip - win.base > 4 * kWave - 8) {
+      win.w = load_word(in, N, ip + 4 * lane);
+      win.base = ip;
+    }
     uint32_t c = win_ld32(win, ip) & 0xff;
-    uint32_t tag = win_ld32(win, ip + 1);                                // :426-430 (zeros past N)
+    uint32_t tag = win_ld32(win, ip + 1);                                // :426-430
     ip += 1;
     uint32_t entry = char_entry(c);                                      // :435-439
     uint32_t len = entry & 0xff;
     uint32_t taglen = entry >> 11;
     uint32_t trailer = taglen >= 4 ? tag : (tag & ((1u << (8 * taglen)) - 1u));
     ip += taglen;
-    if (c & 3) {                                                         // :458-460 copy
+    if (c & 3) {                                                         // :458-460
       uint32_t offset = (entry & 0x700) + trailer;
       int64_t avail_out = (int64_t)size - op;
       if ((int64_t)op <= (int64_t)(uint32_t)(offset - 1u)) return kErrCopyOffset;   // :499
-      if (!(len <= 16 && offset >= 8 && avail_out >= 16) && avail_out < (int64_t)len)
-        return kErrCopyLength;                                           // :505
+      if (!(len <= 16 && offset >= 8 && avail_out >= 16) && avail_out < (int64_t)len) return kErrCopyLength;
       if (lane < len) {
-        uint32_t k = lane;
-        uint32_t sidx = op - offset + (offset >= len ? k : k % offset);
-        if (kLds) {
-          out[op + k] = out[sidx];
-        } else {
-          volatile uint8_t* vo = out;
-          vo[op + k] = vo[sidx];
-        }
+        uint32_t sidx = op - offset + (offset >= len ? lane : lane % offset);
+        vo[op + lane] = vo[sidx];
       }
-      if (!kLds) __threadfence_block();
+      __threadfence_block();
       op += len;
-    } else {                                                             // :461-462 literal
-      uint32_t litlen = len + trailer;                                   // UInt32 wrap
+    } else {                                                             // :461-462
+      uint32_t litlen = len + trailer;
       int64_t avail_out = (int64_t)size - op;
       int64_t avail_in = (int64_t)N - ip;
       if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) return kErrLiteral;  // :518
-      for (uint32_t k = lane; k < litlen; k += kWave) {
-        if (kLds) out[op + k] = in[ip + k];
-        else ((volatile uint8_t*)out)[op + k] = in[ip + k];
-      }
-      if (!kLds) __threadfence_block();
+      for (uint32_t k = lane; k < litlen; k += kWave) vo[op + k] = in[ip + k];
+      __threadfence_block();
       op += litlen;
       ip += litlen;
     }
@@ -99,8 +109,248 @@ __device__ inline int32_t decode_stream(const uint8_t* __restrict__ in, uint32_t
   return kOk;
 }
 
+// ---------------------------------------------------------------------------------------
+// batched tag engine
+
+// write the low `cnt` (0..8) bytes of v at out[o] (global)
+__device__ inline void store_partial(uint8_t* out, uint32_t o, uint64_t v, uint32_t cnt) {
+  if (cnt >= 8) {
+    *reinterpret_cast<du64u*>(out + o) = v;
+    return;
+  }
+  if (cnt & 4) {
+    *reinterpret_cast<du32u*>(out + o) = (uint32_t)v;
+    o += 4;
+    v >>= 32;
+  }
+  if (cnt & 2) {
+    *reinterpret_cast<du16u*>(out + o) = (uint16_t)v;
+    o += 2;
+    v >>= 16;
+  }
+  if (cnt & 1) out[o] = (uint8_t)v;
+}
+
+// size of a tag starting with byte c followed by `trailer` (u8; 255 = long literal)
+__device__ inline uint32_t spec_size(uint32_t c, uint32_t trailer) {
+  uint32_t entry = char_entry(c);
+  uint32_t taglen = entry >> 11;
+  if (c & 3) return 1 + taglen;
+  uint32_t len = entry & 0xff;
+  uint32_t tr = taglen >= 4 ? trailer : (trailer & ((1u << (8 * taglen)) - 1u));
+  uint32_t lit = len + tr;  // u32 wrap, as the reference
+  return lit > 200 ? 255u : 1 + taglen + lit;
+}
+
+__device__ inline uint32_t pack_sizes(uint32_t cur, uint32_t nxt) {
+  uint32_t s = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t c = (cur >> (8 * j)) & 0xff;
+    uint32_t tr = j == 3 ? nxt : __builtin_amdgcn_alignbyte(nxt, cur, j + 1);
+    s |= spec_size(c, tr) << (8 * j);
+  }
+  return s;
+}
+
+// ring slot write: stream bytes [base, base+256) (word per lane) at ring[(base & 1023)]
+__device__ inline void ring_put(uint8_t* ring, uint32_t base, uint32_t word, uint32_t lane) {
+  uint32_t r = base & (kRing - 1);
+  reinterpret_cast<uint32_t*>(ring + r)[lane] = word;
+  if (r == 0 && lane < 4) reinterpret_cast<uint32_t*>(ring + kRing)[lane] = word;  // mirror
+}
+
+__device__ inline uint64_t ring_get8(const uint8_t* ring, uint32_t pos) {
+  return *reinterpret_cast<const du64u*>(ring + (pos & (kRing - 1)));
+}
+
+__device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t size,
+                                       uint8_t* out, uint8_t* ring, uint32_t lane) {
+  // ring holds stream bytes [wb, wb+768); wpre = [wb+768, wb+1024) in flight
+  uint32_t wb = ip & ~255u;
+  ring_put(ring, wb, load_word(in, N, wb + 4 * lane), lane);
+  ring_put(ring, wb + 256, load_word(in, N, wb + 256 + 4 * lane), lane);
+  ring_put(ring, wb + 512, load_word(in, N, wb + 512 + 4 * lane), lane);
+  uint32_t wpre = load_word(in, N, wb + 768 + 4 * lane);
+  uint32_t op = 0;
+  const int64_t Nm1 = (int64_t)N - 1;
+
+  while ((int64_t)ip < Nm1) {
+    if (ip >= wb + 256) {
+      if (ip < wb + 512) {
+        ring_put(ring, wb + 768, wpre, lane);
+        wb += 256;
+        wpre = load_word(in, N, wb + 768 + 4 * lane);
+      } else {  // jumped (long literal): refill
+        wb = ip & ~255u;
+        ring_put(ring, wb, load_word(in, N, wb + 4 * lane), lane);
+        ring_put(ring, wb + 256, load_word(in, N, wb + 256 + 4 * lane), lane);
+        ring_put(ring, wb + 512, load_word(in, N, wb + 512 + 4 * lane), lane);
+        wpre = load_word(in, N, wb + 768 + 4 * lane);
+      }
+    }
+    // speculative sizes for positions [wb, wb+256)
+    const uint64_t cw = ring_get8(ring, wb + 4 * lane);
+    const uint32_t sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
+
+    // walk (wave-uniform scalar)
+    uint32_t ntok = 0, tpos = 0, ipw = ip;
+    bool big = false;
+    const uint32_t wlim = (int64_t)(wb + 256) < Nm1 ? wb + 256 : (uint32_t)Nm1;  // N >= 2 here
+    while (ntok < 64 && ipw < wlim) {
+      uint32_t rel = ipw - wb;
+      uint32_t s = (readlane(sizes, rel >> 2) >> ((rel & 3) * 8)) & 0xff;
+      if (s == 255) {
+        big = true;
+        break;
+      }
+      tpos = lane == ntok ? ipw : tpos;
+      ++ntok;
+      ipw += s;
+    }
+
+    if (ntok) {
+      const bool mine = lane < ntok;
+      const uint64_t hv = ring_get8(ring, mine ? tpos : wb);
+      const uint32_t c = (uint32_t)hv & 0xff;
+      const uint32_t entry = char_entry(c);
+      const uint32_t len = entry & 0xff;
+      const uint32_t taglen = entry >> 11;
+      const uint32_t tr_raw = (uint32_t)(hv >> 8);
+      const uint32_t trailer = taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * taglen)) - 1u));
+      const bool iscopy = (c & 3) != 0;
+      const uint32_t offset = (entry & 0x700) + trailer;
+      const uint32_t litlen = len + trailer;
+      const uint32_t olen = iscopy ? len : litlen;
+      const uint32_t osat = mine ? min(olen, 65537u) : 0u;
+      const uint32_t incl = wave_incl_scan(osat, lane);
+      const uint32_t opt = op + incl - osat;
+      const uint32_t lsrc = tpos + 1 + taglen;
+      int32_t err = kOk;
+      if (mine) {
+        int64_t avail_out = (int64_t)size - (int64_t)opt;
+        if (iscopy) {
+          if ((int64_t)opt <= (int64_t)(uint32_t)(offset - 1u)) err = kErrCopyOffset;                    // :499
+          else if (!(len <= 16 && offset >= 8 && avail_out >= 16) && avail_out < (int64_t)len) err = kErrCopyLength;  // :505
+        } else {
+          int64_t avail_in = (int64_t)N - (int64_t)lsrc;
+          if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) err = kErrLiteral;             // :518
+        }
+      }
+      const uint64_t em = ballot(err != kOk);
+      if (em) return (int32_t)readlane((uint32_t)err, ctz64(em));
+
+      // dependencies: tfirst = last tag u < t whose output starts at or before the source start
+      const uint32_t O0 = op;
+      const uint32_t slo = opt - offset;
+      const uint32_t shi = slo + min(len, offset);
+      uint32_t lo = 0, hi = lane ? lane - 1 : 0;
+#pragma unroll
+      for (int it = 0; it < 6; ++it) {
+        uint32_t mid = (lo + hi + 1) >> 1;
+        uint32_t om = __shfl(opt, mid, 64);
+        if (lo < hi) {
+          if (om <= slo) lo = mid;
+          else hi = mid - 1;
+        }
+      }
+      const uint32_t tfirst = lo;
+      const uint64_t all = ntok == 64 ? ~0ull : ((1ull << ntok) - 1);
+      const bool longlit = !iscopy && litlen > 64;
+      uint64_t done = (ballot(longlit) & all) | ~all;
+
+      // long literals (no dependencies): whole-wave copies from HBM
+      uint64_t lm = ballot(mine && longlit);
+      while (lm) {
+        uint32_t t = ctz64(lm);
+        lm &= lm - 1;
+        uint32_t o = readlane(opt, t), s = readlane(lsrc, t), L = readlane(litlen, t);
+        for (uint32_t k = lane; k < L; k += kWave) out[o + k] = in[s + k];
+      }
+
+      const uint64_t range = lane > tfirst ? (((1ull << lane) - 1) & ~((1ull << tfirst) - 1)) : 0ull;
+      const uint32_t eff = offset >= 8 ? offset : offset * ((8 + offset - 1) / offset);
+      bool need_fence = true;  // earlier batches' stores must land before copies read them
+      while (done != ~0ull) {
+        if (need_fence) __threadfence_block();
+        need_fence = true;
+        bool ready = !((done >> lane) & 1) && (!iscopy || shi <= O0 || ((~done) & range) == 0);
+        uint64_t rm = ballot(ready);
+        if (ready) {
+          if (!iscopy) {
+            for (uint32_t i = 0; i < litlen; i += 8)
+              store_partial(out, opt + i, ring_get8(ring, lsrc + i), litlen - i);
+          } else {
+            uint32_t i = 0;
+            if (offset < 8) {
+              uint64_t x = *reinterpret_cast<const du64u*>(out + slo);
+              uint64_t pat = x & ((1ull << (8 * offset)) - 1);
+              for (uint32_t have = offset; have < 8; have *= 2) pat |= pat << (8 * have);
+              store_partial(out, opt, pat, len);
+              i = 8;
+            }
+            for (; i < len; i += 8) {
+              if (eff < len) __threadfence_block();  // source may be this lane's previous chunk
+              store_partial(out, opt + i, *reinterpret_cast<const du64u*>(out + opt + i - eff), len - i);
+            }
+          }
+        }
+        done |= rm;
+      }
+      op += readlane(incl, ntok - 1);
+      ip = ipw;
+    }
+
+    if (big) {
+      // one literal too long for the batch path (or a wrapped length): scalar decode
+      const uint64_t hv = ring_get8(ring, ip);
+      const uint32_t c = uniform((uint32_t)hv & 0xff);
+      const uint32_t entry = char_entry(c);
+      const uint32_t taglen = entry >> 11;
+      const uint32_t tr_raw = uniform((uint32_t)(hv >> 8));
+      const uint32_t trailer = taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * taglen)) - 1u));
+      const uint32_t litlen = (entry & 0xff) + trailer;
+      const uint32_t lsrc = ip + 1 + taglen;
+      const int64_t avail_out = (int64_t)size - (int64_t)op;
+      const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
+      if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) return kErrLiteral;  // :518
+      // bulk copy HBM -> LDS: head bytes to 16-B source alignment, then 16 B per lane
+      const uint8_t* s = in + lsrc;
+      uint32_t head = (uint32_t)((16 - ((uintptr_t)s & 15)) & 15);
+      if (head > litlen) head = litlen;
+      if (lane < head) out[op + lane] = s[lane];
+      const uint4* s16 = reinterpret_cast<const uint4*>(s + head);
+      const uint32_t n16 = (litlen - head) >> 4;
+      uint8_t* d = out + op + head;
+      uint32_t k = lane;
+      for (; k + 3 * kWave < n16; k += 4 * kWave) {
+        uint4 v0 = s16[k], v1 = s16[k + kWave], v2 = s16[k + 2 * kWave], v3 = s16[k + 3 * kWave];
+        *reinterpret_cast<du64u*>(d + 16 * k) = ((uint64_t)v0.y << 32) | v0.x;
+        *reinterpret_cast<du64u*>(d + 16 * k + 8) = ((uint64_t)v0.w << 32) | v0.z;
+        *reinterpret_cast<du64u*>(d + 16 * (k + kWave)) = ((uint64_t)v1.y << 32) | v1.x;
+        *reinterpret_cast<du64u*>(d + 16 * (k + kWave) + 8) = ((uint64_t)v1.w << 32) | v1.z;
+        *reinterpret_cast<du64u*>(d + 16 * (k + 2 * kWave)) = ((uint64_t)v2.y << 32) | v2.x;
+        *reinterpret_cast<du64u*>(d + 16 * (k + 2 * kWave) + 8) = ((uint64_t)v2.w << 32) | v2.z;
+        *reinterpret_cast<du64u*>(d + 16 * (k + 3 * kWave)) = ((uint64_t)v3.y << 32) | v3.x;
+        *reinterpret_cast<du64u*>(d + 16 * (k + 3 * kWave) + 8) = ((uint64_t)v3.w << 32) | v3.z;
+      }
+      for (; k < n16; k += kWave) {
+        uint4 v0 = s16[k];
+        *reinterpret_cast<du64u*>(d + 16 * k) = ((uint64_t)v0.y << 32) | v0.x;
+        *reinterpret_cast<du64u*>(d + 16 * k + 8) = ((uint64_t)v0.w << 32) | v0.z;
+      }
+      const uint32_t done16 = head + (n16 << 4);
+      if (lane < litlen - done16) out[op + done16 + lane] = s[done16 + lane];
+      op += litlen;
+      ip = lsrc + litlen;
+    }
+  }
+  if (op != size) return kErrInvalid;                                    // Snappy.jl:50
+  return kOk;
+}
+
 __global__ __launch_bounds__(64) void k_decompress(DecompressArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t sout[kBlockSize + 64];
+  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
   const uint8_t* in = a.in + a.in_off[b];
@@ -117,22 +367,25 @@ __global__ __launch_bounds__(64) void k_decompress(DecompressArgs a) {
     uint32_t bt = readlane(hb, i);
     if (i < 4) {
       size |= (bt & 0x7f) << (7 * i);
-      if (bt < 0x80) { st = kOk; ip = i + 1; break; }
+      if (bt < 0x80) {
+        st = kOk;
+        ip = i + 1;
+        break;
+      }
     } else {
       size |= (bt & 0x7f) << 28;
-      if (bt < 0x10) { st = kOk; ip = 5; }
+      if (bt < 0x10) {
+        st = kOk;
+        ip = 5;
+      }
     }
   }
   if (st == kOk && size > cap) st = kBufferTooSmall;
   if (st == kOk) {
     if (size <= kBlockSize) {
-      st = decode_stream<true>(in, N, ip, size, sout, lane);
-      if (st == kOk) {
-        __syncthreads();
-        wave_copy_lds_to_global(dst, sout, 0, size, lane);
-      }
+      st = decode_stream_batch(in, N, ip, size, dst, sring, lane);
     } else {
-      st = decode_stream<false>(in, N, ip, size, dst, lane);
+      st = decode_stream_global(in, N, ip, size, dst, lane);
     }
   }
   if (lane == 0) {

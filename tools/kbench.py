@@ -1,0 +1,52 @@
+"""Kernel driver for profiling (rocprofv3 --kernel-trace / --pmc): runs one codec kernel R
+times on the bench workload (text or random 64 KiB blocks), device-resident.
+
+  python tools/kbench.py --op compress_fast|compress_ref|uncompress --blocks 2000 --reps 5 [--data random]
+"""
+import argparse
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--op", default="compress_fast")
+    ap.add_argument("--blocks", type=int, default=2000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--data", default="text")
+    args = ap.parse_args()
+    sm = bench.load_package()
+    dev = torch.device("cuda", 0)
+    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 7)
+    b = bench.Batch(blocks, dev)
+    b.compress(sm, "fast")
+    torch.cuda.synchronize()
+    ops = {
+        "compress_fast": lambda: b.compress(sm, "fast"),
+        "compress_ref": lambda: b.compress(sm, "reference"),
+        "uncompress": lambda: b.uncompress(sm),
+    }
+    fn = ops[args.op]
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        fn()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.reps
+    nbytes = args.blocks * bench.BLOCK
+    print("%s %s: %.3f ms/launch, %.2f GB/s (uncompressed bytes), ratio %.4f" % (
+        args.op, args.data, dt * 1e3, nbytes / dt / 1e9, float(b.comp_len.sum()) / nbytes))
+    if args.op == "uncompress":
+        print("roundtrip ok:", b.verify())
+
+
+if __name__ == "__main__":
+    main()
