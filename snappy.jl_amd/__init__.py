@@ -26,7 +26,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsnappy_mi355x.so")
+# SNAPPY_MI355X_LIB: alternate build of the same library (diagnostic/ablation builds only)
+LIB_PATH = os.environ.get("SNAPPY_MI355X_LIB") or os.path.join(HERE, "libsnappy_mi355x.so")
 BLOCK_SIZE = 65536
 
 SM_OK = 0

@@ -32,6 +32,10 @@
 #include "sm_device.h"
 #include "sm_internal.h"
 
+#ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only)
+#define SM_ABLATE_D 0
+#endif
+
 namespace sm {
 
 typedef uint16_t __attribute__((aligned(1))) du16u;
@@ -165,48 +169,108 @@ __device__ inline uint64_t ring_get8(const uint8_t* ring, uint32_t pos) {
 }
 
 __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t size,
-                                       uint8_t* out, uint8_t* ring, uint32_t lane) {
-  // ring holds stream bytes [wb, wb+768); wpre = [wb+768, wb+1024) in flight
+                                       uint8_t* out, uint8_t* ring, uint16_t* jt, uint32_t lane) {
+  // ring holds stream bytes [wb, wb+768); pre1 = [wb+768, wb+1024) (loaded a batch ago),
+  // pre2 = [wb+1024, wb+1280) issued at the end of the previous batch -- so a round's fence
+  // (s_waitcnt vmcnt(0)) never waits for a freshly issued prefetch.
   uint32_t wb = ip & ~255u;
   ring_put(ring, wb, load_word(in, N, wb + 4 * lane), lane);
   ring_put(ring, wb + 256, load_word(in, N, wb + 256 + 4 * lane), lane);
   ring_put(ring, wb + 512, load_word(in, N, wb + 512 + 4 * lane), lane);
-  uint32_t wpre = load_word(in, N, wb + 768 + 4 * lane);
+  uint32_t pre1 = load_word(in, N, wb + 768 + 4 * lane);
+  uint32_t pre2 = load_word(in, N, wb + 1024 + 4 * lane);
+  bool issue_pre2 = false;
   uint32_t op = 0;
   const int64_t Nm1 = (int64_t)N - 1;
 
   while ((int64_t)ip < Nm1) {
     if (ip >= wb + 256) {
       if (ip < wb + 512) {
-        ring_put(ring, wb + 768, wpre, lane);
+        ring_put(ring, wb + 768, pre1, lane);
+        pre1 = pre2;
         wb += 256;
-        wpre = load_word(in, N, wb + 768 + 4 * lane);
+        issue_pre2 = true;  // [wb+1024, wb+1280) loads after this batch
       } else {  // jumped (long literal): refill
         wb = ip & ~255u;
         ring_put(ring, wb, load_word(in, N, wb + 4 * lane), lane);
         ring_put(ring, wb + 256, load_word(in, N, wb + 256 + 4 * lane), lane);
         ring_put(ring, wb + 512, load_word(in, N, wb + 512 + 4 * lane), lane);
-        wpre = load_word(in, N, wb + 768 + 4 * lane);
+        pre1 = load_word(in, N, wb + 768 + 4 * lane);
+        pre2 = load_word(in, N, wb + 1024 + 4 * lane);
+        issue_pre2 = false;
       }
     }
-    // speculative sizes for positions [wb, wb+256)
+    // speculative tag sizes for positions [wb, wb+256)
     const uint64_t cw = ring_get8(ring, wb + 4 * lane);
     const uint32_t sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
 
-    // walk (wave-uniform scalar)
-    uint32_t ntok = 0, tpos = 0, ipw = ip;
-    bool big = false;
-    const uint32_t wlim = (int64_t)(wb + 256) < Nm1 ? wb + 256 : (uint32_t)Nm1;  // N >= 2 here
-    while (ntok < 64 && ipw < wlim) {
-      uint32_t rel = ipw - wb;
-      uint32_t s = (readlane(sizes, rel >> 2) >> ((rel & 3) * 8)) & 0xff;
-      if (s == 255) {
-        big = true;
-        break;
+    // Parallel tag walk by pointer doubling over the 256 window positions (VALU + LDS, no
+    // serial SALU loop).  J0[p] = p + size(p); a position whose tag is a long literal, or that
+    // lies at/after the parse limit (window end or N-1, internal.jl:416), is a stop node
+    // (J0[p] = p, self-loop).  J_k = J_{k-1} o J_{k-1} (k < 8; sizes >= 2 so a window holds
+    // <= 128 tags).  Position p is a tag start iff the binary descent from the window's first
+    // tag s0 along J_7..J_0 (largest chain element <= p) lands on p.
+    const uint32_t wlim = (int64_t)(wb + 256) < Nm1 ? wb + 256 : (uint32_t)Nm1;
+    const uint32_t rlim = wlim - wb;
+    const uint32_t s0 = ip - wb;
+    uint32_t J[4], nxt[4];
+    bool stopn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t p = 4 * lane + j;
+      const uint32_t sz = (sizes >> (8 * j)) & 0xff;
+      stopn[j] = sz == 255 || p >= rlim;
+      nxt[j] = p + sz;
+      J[j] = stopn[j] ? p : p + sz;
+    }
+    uint16_t* jt0 = jt;
+    *reinterpret_cast<uint2*>(jt0 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const uint16_t* prev = jt + (k - 1) * 256;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) J[j] = J[j] < 256 ? prev[J[j]] : J[j];
+      *reinterpret_cast<uint2*>(jt + k * 256 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+    }
+    uint32_t cur[4] = {s0, s0, s0, s0};
+#pragma unroll
+    for (int k = 7; k >= 0; --k) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t t = jt[k * 256 + cur[j]];
+        cur[j] = t <= 4 * lane + j ? t : cur[j];
       }
-      tpos = lane == ntok ? ipw : tpos;
-      ++ntok;
-      ipw += s;
+    }
+    bool isv[4];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t p = 4 * lane + j;
+      isv[j] = cur[j] == p && p >= s0 && !stopn[j];  // a tag of this batch
+      cnt += isv[j] ? 1u : 0u;
+    }
+    const uint32_t rank0 = scan_dpp(cnt) - cnt;
+    const uint32_t nvalid = readlane(rank0 + cnt, 63);
+    // compact: slot[rank] = p | next << 16 (slots 0..63; reuses jt level 0, no longer read)
+    {
+      uint32_t rk = rank0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (isv[j] && rk < 64) reinterpret_cast<uint32_t*>(jt)[rk] = (4 * lane + j) | (nxt[j] << 16);
+        rk += isv[j] ? 1u : 0u;
+      }
+    }
+    const uint32_t ntok = nvalid < 64 ? nvalid : 64;
+    uint32_t tpos = 0, ipw = ip;
+    bool big = false;
+    if (ntok) {
+      const uint32_t sv = reinterpret_cast<const uint32_t*>(jt)[lane < ntok ? lane : 0];
+      tpos = wb + (sv & 0xffff);
+      ipw = wb + readlane(sv >> 16, ntok - 1);
+    }
+    if (ipw < wlim) {
+      const uint32_t rel = ipw - wb;
+      big = ((readlane(sizes, rel >> 2) >> ((rel & 3) * 8)) & 0xff) == 255;
     }
 
     if (ntok) {
@@ -223,17 +287,17 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const uint32_t litlen = len + trailer;
       const uint32_t olen = iscopy ? len : litlen;
       const uint32_t osat = mine ? min(olen, 65537u) : 0u;
-      const uint32_t incl = wave_incl_scan(osat, lane);
+      const uint32_t incl = scan_dpp(osat);
       const uint32_t opt = op + incl - osat;
       const uint32_t lsrc = tpos + 1 + taglen;
       int32_t err = kOk;
       if (mine) {
-        int64_t avail_out = (int64_t)size - (int64_t)opt;
+        const int64_t avail_out = (int64_t)size - (int64_t)opt;
         if (iscopy) {
           if ((int64_t)opt <= (int64_t)(uint32_t)(offset - 1u)) err = kErrCopyOffset;                    // :499
           else if (!(len <= 16 && offset >= 8 && avail_out >= 16) && avail_out < (int64_t)len) err = kErrCopyLength;  // :505
         } else {
-          int64_t avail_in = (int64_t)N - (int64_t)lsrc;
+          const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
           if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) err = kErrLiteral;             // :518
         }
       }
@@ -247,8 +311,8 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       uint32_t lo = 0, hi = lane ? lane - 1 : 0;
 #pragma unroll
       for (int it = 0; it < 6; ++it) {
-        uint32_t mid = (lo + hi + 1) >> 1;
-        uint32_t om = __shfl(opt, mid, 64);
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        const uint32_t om = __shfl(opt, mid, 64);
         if (lo < hi) {
           if (om <= slo) lo = mid;
           else hi = mid - 1;
@@ -259,46 +323,90 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const bool longlit = !iscopy && litlen > 64;
       uint64_t done = (ballot(longlit) & all) | ~all;
 
-      // long literals (no dependencies): whole-wave copies from HBM
+      // long literals (65..200 B, no dependencies, still inside the ring window): one whole-wave
+      // pass each, 8 bytes per lane
       uint64_t lm = ballot(mine && longlit);
       while (lm) {
-        uint32_t t = ctz64(lm);
+        const uint32_t t = ctz64(lm);
         lm &= lm - 1;
-        uint32_t o = readlane(opt, t), s = readlane(lsrc, t), L = readlane(litlen, t);
-        for (uint32_t k = lane; k < L; k += kWave) out[o + k] = in[s + k];
+        const uint32_t o = readlane(opt, t), s = readlane(lsrc, t), L = readlane(litlen, t);
+        const uint32_t k = 8 * lane;
+        if (k < L) store_partial(out, o + k, ring_get8(ring, s + k), L - k);
       }
 
+      // Dependency rounds.  Every tag of a round issues all its loads before any store:
+      //  * literal (<= 64 B): 8-byte pieces of the LDS ring;
+      //  * copy: its source window S = out[slo, slo+offset) is final when the round starts, and
+      //    output byte j is S[j mod offset] (incremental_copy_slow!, internal.jl:477-481), so
+      //    chunk i = S from phase m = 8i mod offset, wrapping once to S's start (offset >= 8);
+      //    for offset < 8 the period is unrolled to 16 bytes in registers.
       const uint64_t range = lane > tfirst ? (((1ull << lane) - 1) & ~((1ull << tfirst) - 1)) : 0ull;
-      const uint32_t eff = offset >= 8 ? offset : offset * ((8 + offset - 1) / offset);
-      bool need_fence = true;  // earlier batches' stores must land before copies read them
+      if (SM_ABLATE_D & 1) done = ~0ull;
       while (done != ~0ull) {
-        if (need_fence) __threadfence_block();
-        need_fence = true;
-        bool ready = !((done >> lane) & 1) && (!iscopy || shi <= O0 || ((~done) & range) == 0);
-        uint64_t rm = ballot(ready);
-        if (ready) {
-          if (!iscopy) {
-            for (uint32_t i = 0; i < litlen; i += 8)
-              store_partial(out, opt + i, ring_get8(ring, lsrc + i), litlen - i);
-          } else {
-            uint32_t i = 0;
-            if (offset < 8) {
-              uint64_t x = *reinterpret_cast<const du64u*>(out + slo);
-              uint64_t pat = x & ((1ull << (8 * offset)) - 1);
-              for (uint32_t have = offset; have < 8; have *= 2) pat |= pat << (8 * have);
-              store_partial(out, opt, pat, len);
-              i = 8;
+        __threadfence_block();  // this wave's earlier stores land before the loads below
+        const bool ready = !((done >> lane) & 1) && (!iscopy || shi <= O0 || ((~done) & range) == 0);
+        const uint64_t rm = ballot(ready);
+        const uint32_t L = iscopy ? len : litlen;
+        for (uint32_t base = 0; base < 64; base += 32) {
+          const bool act = ready && L > base;
+          if (!ballot(act)) break;
+          if (act) {
+            uint64_t v[4];
+            if (!iscopy) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+                v[i] = base + 8 * i < L ? ring_get8(ring, lsrc + base + 8 * i) : 0ull;
+            } else if (offset >= 8) {
+              const uint64_t B = *reinterpret_cast<const du64u*>(out + slo);
+              uint32_t m0 = base;
+              while (m0 >= offset) m0 -= offset;
+              uint32_t m = m0;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                v[i] = base + 8 * i < L ? *reinterpret_cast<const du64u*>(out + slo + m) : 0ull;
+                m += 8;
+                if (m >= offset) m -= offset;
+              }
+              m = m0;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const uint32_t keep = offset - m;  // bytes of this chunk before S wraps
+                if (keep < 8) v[i] = (v[i] & ((1ull << (8 * keep)) - 1)) | (B << (8 * keep));
+                m += 8;
+                if (m >= offset) m -= offset;
+              }
+            } else {
+              const uint64_t x = *reinterpret_cast<const du64u*>(out + slo);
+              uint64_t p0 = x & ((1ull << (8 * offset)) - 1);
+              for (uint32_t have = offset; have < 8; have *= 2) p0 |= p0 << (8 * have);
+              // p0 = S repeated over 8 bytes; p1 = the next 8 bytes of the period
+              uint32_t e = 8;
+              while (e >= offset) e -= offset;
+              // p1[k] = seq[8+k] = p0[e+k] (e+k < 8) or p0[e+k-offset] (e+k >= 8)
+              const uint64_t hib = e ? ~0ull << (8 * (8 - e)) : 0ull;
+              const uint64_t p1 = e ? ((p0 >> (8 * e)) | ((p0 << (8 * (offset - e))) & hib)) : p0;
+              uint32_t m = base;
+              while (m >= offset) m -= offset;
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                v[i] = m ? ((p0 >> (8 * m)) | (p1 << (8 * (8 - m)))) : p0;
+                m += 8;
+                while (m >= offset) m -= offset;
+              }
             }
-            for (; i < len; i += 8) {
-              if (eff < len) __threadfence_block();  // source may be this lane's previous chunk
-              store_partial(out, opt + i, *reinterpret_cast<const du64u*>(out + opt + i - eff), len - i);
-            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (base + 8 * i < L) store_partial(out, opt + base + 8 * i, v[i], L - base - 8 * i);
           }
         }
         done |= rm;
       }
       op += readlane(incl, ntok - 1);
       ip = ipw;
+    }
+    if (issue_pre2) {
+      pre2 = load_word(in, N, wb + 1024 + 4 * lane);
+      issue_pre2 = false;
     }
 
     if (big) {
@@ -314,7 +422,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const int64_t avail_out = (int64_t)size - (int64_t)op;
       const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
       if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) return kErrLiteral;  // :518
-      // bulk copy HBM -> LDS: head bytes to 16-B source alignment, then 16 B per lane
+      // bulk copy: head bytes to 16-B source alignment, then 16 B per lane, 4 in flight
       const uint8_t* s = in + lsrc;
       uint32_t head = (uint32_t)((16 - ((uintptr_t)s & 15)) & 15);
       if (head > litlen) head = litlen;
@@ -349,8 +457,9 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   return kOk;
 }
 
-__global__ __launch_bounds__(64) void k_decompress(DecompressArgs a) {
+__global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[8 * 256];  // tag-walk jump tables
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
   const uint8_t* in = a.in + a.in_off[b];
@@ -383,7 +492,7 @@ __global__ __launch_bounds__(64) void k_decompress(DecompressArgs a) {
   if (st == kOk && size > cap) st = kBufferTooSmall;
   if (st == kOk) {
     if (size <= kBlockSize) {
-      st = decode_stream_batch(in, N, ip, size, dst, sring, lane);
+      st = decode_stream_batch(in, N, ip, size, dst, sring, sjt, lane);
     } else {
       st = decode_stream_global(in, N, ip, size, dst, lane);
     }

@@ -86,6 +86,17 @@ __device__ inline uint32_t wave_incl_scan(uint32_t v, uint32_t lane) {
   return v;
 }
 
+// inclusive wave-64 scan with DPP (row_shr 1/2/4/8 within rows, row_bcast 15/31 across)
+__device__ inline uint32_t scan_dpp(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xf, 0xf, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xa, 0xf, false);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xc, 0xf, false);
+  return v;
+}
+
 // unaligned little-endian 32-bit load from an LDS byte array (two aligned dword reads +
 // v_alignbyte_b32).  The array must have >= 4 readable bytes past pos+3.
 __device__ inline uint32_t lds_ld32(const uint8_t* lds, uint32_t pos) {
