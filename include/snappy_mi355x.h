@@ -91,6 +91,15 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t compressed_l
 sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
                                    const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                    const uint64_t* d_out_off, uint32_t* d_out_len, int mode, void* stream);
+/* Fragments of ONE stream (the block loop of src/Snappy.jl:29-33): like
+ * sm_compress_batch_device but no per-fragment varint header, and every fragment uses the
+ * hash-table size the reference derives from the stream's total length total_len
+ * (src/Snappy.jl:27, quirk Q2).  The caller writes varint(total_len) and concatenates the
+ * fragments in order (e.g. after a size all-gather across GPUs, snappy.jl_amd/dist.py). */
+sm_status sm_compress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                       const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
+                                       const uint64_t* d_out_off, uint32_t* d_out_len, uint64_t total_len,
+                                       int mode, void* stream);
 /* Block b: compressed stream d_in[d_in_off[b] .. +d_in_len[b]) -> d_out + d_out_off[b] with
  * capacity d_out_cap[b].  d_status[b] = SM_OK or the reference's error code (first error in
  * stream order); d_out_len[b] = decoded bytes (0 on error).  Each block decodes as

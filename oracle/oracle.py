@@ -55,6 +55,8 @@ def lib():
         L.smo_hashtable_size.argtypes = [ctypes.c_size_t]
         L.smo_char_table.restype = ctypes.c_uint16
         L.smo_char_table.argtypes = [ctypes.c_uint8]
+        L.smo_compress_fragment.restype = ctypes.c_int
+        L.smo_compress_fragment.argtypes = [c_u8p, ctypes.c_size_t, c_u8p, ctypes.POINTER(ctypes.c_size_t), ctypes.c_size_t, ctypes.c_int]
         L.smo_compress_batch.restype = ctypes.c_int
         L.smo_compress_batch.argtypes = [c_u8p, c_u8p, c_u8p, ctypes.c_uint32, c_u8p, c_u8p, c_u8p, ctypes.c_int, ctypes.c_int]
         L.smo_uncompress_batch.restype = ctypes.c_int
@@ -83,6 +85,18 @@ def compress(data, compat=False):
     out = np.empty(max_compressed_length(src.size) + 8, dtype=np.uint8)
     ol = ctypes.c_size_t(0)
     st = lib().smo_compress(src.ctypes.data, src.size, out.ctypes.data, ctypes.byref(ol), int(compat))
+    if st:
+        raise OracleError(st)
+    return out[: ol.value].tobytes()
+
+
+def compress_fragment(data, total_len, compat=False):
+    """One <= 64 KiB fragment of a total_len-byte stream, as Snappy.jl's block loop emits it."""
+    src = _buf(data)
+    out = np.empty(max_compressed_length(src.size) + 8, dtype=np.uint8)
+    ol = ctypes.c_size_t(0)
+    st = lib().smo_compress_fragment(src.ctypes.data if src.size else None, src.size, out.ctypes.data,
+                                     ctypes.byref(ol), total_len, int(compat))
     if st:
         raise OracleError(st)
     return out[: ol.value].tobytes()

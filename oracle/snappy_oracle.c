@@ -204,6 +204,18 @@ int smo_compress(const uint8_t* in, size_t n, uint8_t* out, size_t* out_len, int
   return SMO_OK;
 }
 
+/* One fragment of a larger stream, as the block loop of Snappy.jl:29-33 runs it: no header,
+ * table size from the stream's total length (Q2).  n <= 65536. */
+int smo_compress_fragment(const uint8_t* in, size_t n, uint8_t* out, size_t* out_len, size_t total_len,
+                          int compat) {
+  if (n > K_BLOCK_SIZE) return SMO_INVALID_INPUT;
+  uint16_t table[K_MAX_HASH_TABLE_SIZE];
+  uint32_t tsize = compat ? smo_hashtable_size(n) : smo_hashtable_size(total_len);
+  memset(table, 0xff, tsize * sizeof(uint16_t));
+  *out_len = compress_fragment(out, 0, in, 0, (long)n - 1, table, tsize, compat);
+  return SMO_OK;
+}
+
 int smo_uncompressed_length(const uint8_t* in, size_t n, size_t* result) {
   uint32_t v; size_t next;
   int st = smo_parse32(in, n, 0, &v, &next);                 /* Snappy.jl:90-92 */

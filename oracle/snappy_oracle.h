@@ -61,6 +61,9 @@ int smo_compress(const uint8_t* in, size_t n, uint8_t* out, size_t* out_len, int
  * If the declared length exceeds out_cap returns SMO_BUFFER_TOO_SMALL before decoding. */
 int smo_uncompress(const uint8_t* in, size_t n, uint8_t* out, size_t out_cap, size_t* out_len);
 int smo_uncompressed_length(const uint8_t* in, size_t n, size_t* result);
+/* one <= 64 KiB fragment of a stream of total_len bytes (no header; Q2 table size) */
+int smo_compress_fragment(const uint8_t* in, size_t n, uint8_t* out, size_t* out_len, size_t total_len,
+                          int compat);
 
 /* batch helpers used by bench.py's cpu_baseline leg (OpenMP over blocks when nthreads>1) */
 int smo_compress_batch(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,

@@ -39,7 +39,7 @@ ABI_SYMBOLS = (
     "sm_status_message", "sm_max_compressed_length", "sm_uncompressed_length", "sm_parse32",
     "sm_encode32", "sm_ctx_create", "sm_ctx_destroy", "sm_ctx_stream", "sm_compress", "sm_uncompress",
     "sm_compress_batch_device", "sm_uncompress_batch_device", "sm_compress_batch",
-    "sm_uncompress_batch", "sm_version",
+    "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device",
 )
 
 
@@ -97,6 +97,8 @@ def lib():
         L.sm_uncompress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
         L.sm_version.restype = ctypes.c_char_p
         L.sm_version.argtypes = []
+        L.sm_compress_fragments_device.restype = i32
+        L.sm_compress_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp]
         _lib = L
     return _lib
 
@@ -274,6 +276,22 @@ def compress_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len,
     st = lib().sm_compress_batch_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), d_in_len.numel(),
                                         _ptr(d_out), _ptr(d_out_off), _ptr(d_out_len), _mode(mode),
                                         ctypes.c_void_p(stream))
+    if st:
+        raise SnappyError(st)
+
+
+def compress_fragments_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, total_len, mode="fast",
+                              stream=None, device=None):
+    """Fragments of ONE stream of total_len bytes (no per-fragment header; Q2 table size)."""
+    import torch
+    dev = d_in.device.index if device is None else device
+    if stream is None:
+        stream = torch.cuda.current_stream(dev).cuda_stream
+    elif hasattr(stream, "cuda_stream"):
+        stream = stream.cuda_stream
+    st = lib().sm_compress_fragments_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len),
+                                            d_in_len.numel(), _ptr(d_out), _ptr(d_out_off), _ptr(d_out_len),
+                                            int(total_len), _mode(mode), ctypes.c_void_p(stream))
     if st:
         raise SnappyError(st)
 

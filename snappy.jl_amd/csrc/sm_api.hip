@@ -172,6 +172,20 @@ sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint6
   return SM_OK;
 }
 
+sm_status sm_compress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                       const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
+                                       const uint64_t* d_out_off, uint32_t* d_out_len, uint64_t total_len,
+                                       int mode, void* stream) {
+  if (!ctx || (mode != SM_MODE_REFERENCE && mode != SM_MODE_FAST)) return SM_ERR_ARGUMENT;
+  if (total_len > 0xffffffffull) return SM_ERR_INPUT_TOO_LARGE;        // src/Snappy.jl:21
+  if (nblk == 0) return SM_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return SM_ERR_ARGUMENT;
+  DeviceGuard g(ctx->device);
+  sm::CompressArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nblk, sm::hashtable_size(total_len), 0};
+  SM_CHECK(sm::launch_compress(a, mode, (hipStream_t)stream));
+  return SM_OK;
+}
+
 sm_status sm_uncompress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
                                      const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                      const uint64_t* d_out_off, const uint32_t* d_out_cap,

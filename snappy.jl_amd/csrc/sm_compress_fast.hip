@@ -125,6 +125,7 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
   const uint32_t lane = tid & 63;
   uint32_t* P = T + kFTab + wave * kPriv;                                     // private table
   uint32_t* csize = T + kFTab + kWavesPerBlock * kPriv;                       // per-wave chunk sizes
+  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + kWavesPerBlock) + wave * 8 * kChunk;  // parse jump tables
 
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.in_len[b];
@@ -206,8 +207,7 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
     uint32_t ta = 0, tb = 0, ntok = 0, incl = 0, sz = 0, litlen = 0, littag = 0, ls = 0;
     uint64_t ts0 = 0, ts1 = 0;
     if (active) {
-      uint32_t mlc[2];
-      uint64_t mask[2];
+      uint32_t Ls[2], offs[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t q = c0 + 64 * j + lane;
@@ -221,38 +221,83 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
         const uint32_t la = oka ? 4 + min(ext16(data, ca, q), cap) : 0;
         const uint32_t lb = okb ? 4 + min(ext16(data, cb, q), cap) : 0;
         const bool useb = lb > la;
-        const uint32_t L = useb ? lb : la;
-        const uint32_t c = useb ? cb : ca;
-        mlc[j] = (L << 16) | (q - c);
-        mask[j] = (SM_ABLATE & 2) ? 0ull : ballot(L != 0);
+        Ls[j] = (SM_ABLATE & 2) ? 0u : (useb ? lb : la);
+        offs[j] = q - (useb ? cb : ca);
       }
-      // greedy walk (SALU)
-      uint32_t p = c0;
+      // finish matches that filled the eager window: 8 bytes per lane per step
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const uint32_t s0 = c0 + 64 * j;
-        uint64_t ts = 0;
-        while (p < s0 + 64) {
-          const uint32_t rel = p > s0 ? p - s0 : 0;
-          const uint64_t mm = mask[j] >> rel;
-          if (!mm) break;
-          const uint32_t l = rel + ctz64(mm);
-          const uint32_t q = s0 + l;
-          const uint32_t pk = readlane(mlc[j], l);
-          uint32_t L = pk >> 16;
-          const uint32_t off = pk & 0xffff;
-          if (L >= 4 + kEager && q + L < ce) L += wave_match_len8(data, q - off + L, q + L, ce - q - L, lane);
-          const bool me = lane == ntok;
-          ta = me ? ((q - c0) | (L << 16)) : ta;  // chunk-relative start (ce-c0 can be 128)
-          tb = me ? off : tb;
-          ts |= 1ull << l;
-          ++ntok;
-          p = q + L;
+        const uint32_t q = c0 + 64 * j + lane;
+        uint32_t L = Ls[j];
+        bool more = L >= 4 + kEager && q + L < ce;
+        while (ballot(more)) {
+          if (more) {
+            const uint32_t avail = ce - q - L;
+            const uint64_t x = ld64u(data + q - offs[j] + L) ^ ld64u(data + q + L);
+            const uint32_t fb = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
+            L += min(fb, avail);
+            more = fb == 8 && avail > 8;
+          }
         }
-        if (j == 0) ts0 = ts;
-        else ts1 = ts;
+        Ls[j] = L;
       }
-      if (p < ce) {  // trailing literal run: a token without a copy
+      // Greedy parse by pointer doubling (no serial loop): J0[r] = r + max(L(r), 1) over the
+      // chunk's 128 positions, J_k = J_{k-1} o J_{k-1}; position r is visited by the greedy
+      // walk from 0 iff the binary descent along J_7..J_0 (largest visited position <= r)
+      // lands on r.  Visited match positions are the copies.
+      uint32_t cur[2] = {0xffffu, 0xffffu};  // no copies at all (incompressible): skip the parse
+      if (ballot(Ls[0] != 0 || Ls[1] != 0)) {
+        uint32_t jv[2];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const uint32_t r = 64 * j + lane;
+          jv[j] = r + max(Ls[j], 1u);  // <= 255
+          jt[r] = (uint8_t)jv[j];
+        }
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            jv[j] = jv[j] < kChunk ? jt[(k - 1) * kChunk + jv[j]] : jv[j];
+            jt[k * kChunk + 64 * j + lane] = (uint8_t)jv[j];
+          }
+        }
+        cur[0] = cur[1] = 0;
+#pragma unroll
+        for (int k = 7; k >= 0; --k) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint32_t t = jt[k * kChunk + cur[j]];
+            cur[j] = t <= 64u * j + lane ? t : cur[j];
+          }
+        }
+      }
+      const bool tok0 = cur[0] == lane && Ls[0] != 0;
+      const bool tok1 = cur[1] == 64 + lane && Ls[1] != 0;
+      ts0 = ballot(tok0);
+      ts1 = ballot(tok1);
+      const uint32_t n0 = __builtin_popcountll(ts0);
+      const uint32_t nmatch = n0 + __builtin_popcountll(ts1);
+      uint32_t last_end = 0;
+      if (nmatch) {  // end of the last copy (highest token position)
+        const uint32_t j = ts1 ? 1u : 0u;
+        const uint64_t m = ts1 ? ts1 : ts0;
+        const uint32_t l = 63 - (uint32_t)__builtin_clzll(m);
+        last_end = 64 * j + l + readlane(j ? Ls[1] : Ls[0], l);
+      }
+      // compact the copies into lanes 0..nmatch-1 (slots reuse J level 0..3, no longer read)
+      uint2* slots = reinterpret_cast<uint2*>(jt);
+      if (tok0) slots[__builtin_amdgcn_mbcnt_hi((uint32_t)(ts0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ts0, 0u))] =
+          make_uint2(lane | (Ls[0] << 16), offs[0]);
+      if (tok1) slots[n0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(ts1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ts1, 0u))] =
+          make_uint2((64 + lane) | (Ls[1] << 16), offs[1]);
+      if (lane < nmatch) {
+        const uint2 sv = slots[lane];
+        ta = sv.x;
+        tb = sv.y;
+      }
+      ntok = nmatch;
+      if (last_end < ce - c0) {  // trailing literal run: a token without a copy
         const bool me = lane == ntok;
         ta = me ? ce - c0 : ta;
         tb = me ? 0u : tb;
@@ -332,7 +377,8 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
   if (tid == 0) a.out_len[b] = op;
 }
 
-constexpr size_t kFastLds = kBlockSize + 4 * (kFTab + kWavesPerBlock * kPriv + kWavesPerBlock);
+constexpr size_t kFastLds =
+    kBlockSize + 4 * (kFTab + kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * 8 * kChunk;
 
 hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s) {
   static bool attr_set = false;

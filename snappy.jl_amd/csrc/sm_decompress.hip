@@ -344,7 +344,8 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       if (SM_ABLATE_D & 1) done = ~0ull;
       while (done != ~0ull) {
         __threadfence_block();  // this wave's earlier stores land before the loads below
-        const bool ready = !((done >> lane) & 1) && (!iscopy || shi <= O0 || ((~done) & range) == 0);
+        const bool ready = !((done >> lane) & 1) &&
+                           ((SM_ABLATE_D & 2) || !iscopy || shi <= O0 || ((~done) & range) == 0);
         const uint64_t rm = ballot(ready);
         const uint32_t L = iscopy ? len : litlen;
         for (uint32_t base = 0; base < 64; base += 32) {

@@ -1,0 +1,94 @@
+"""Multi-GPU sharding of the block codec: one process per GPU, torch.distributed (RCCL on
+ROCm; gloo in the CPU tests).
+
+The reference is single-threaded; its 64 KiB fragments are independent
+(src/Snappy.jl:29-33, src/internal.jl:129,190 -- the table is reset and offsets are
+block-relative), so the path shards with no data-path collective:
+
+* batch mode (BASELINE configs 2-4): rank r owns its own contiguous run of independent
+  blocks; nothing is exchanged.  `gather_sizes` is only needed when a global index of the
+  compressed blocks is wanted.
+* one large stream (config 5): fragments [lo, hi) of the stream go to each rank; each rank
+  compresses its fragments (no per-fragment header, table size from the TOTAL length, Q2);
+  one all-gather of the u32 fragment sizes gives every rank the global exclusive scan, i.e.
+  where its fragments land after the varint(total) header.  That all-gather is the only
+  collective on the path (10,304 fragments x 4 B for 644 MiB).
+
+The per-rank compressor is injected (`compress_fn`) so that the CPU tests can run the
+distributed logic with gloo, using the oracle as a stand-in for the GPU kernels.
+"""
+import numpy as np
+
+BLOCK = 65536
+
+
+def shard_range(nitems, rank, world):
+    """Contiguous [lo, hi) of nitems for rank (the first nitems % world ranks get one more)."""
+    base, extra = divmod(nitems, world)
+    lo = rank * base + min(rank, extra)
+    hi = lo + base + (1 if rank < extra else 0)
+    return lo, hi
+
+
+def fragment_bounds(total_len):
+    """(offset, length) of every 64 KiB fragment of a stream (src/Snappy.jl:29)."""
+    nfrag = (total_len + BLOCK - 1) // BLOCK
+    offs = np.arange(nfrag, dtype=np.int64) * BLOCK
+    lens = np.minimum(BLOCK, total_len - offs).astype(np.int64)
+    return offs, lens
+
+
+def varint32(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7F) | 0x80)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def gather_sizes(local_sizes, group=None):
+    """All-gather per-rank u32 size vectors (ragged) -> one global int64 vector, rank order.
+
+    local_sizes: 1-D torch tensor on the device of the process group's backend."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    n = torch.tensor([local_sizes.numel()], dtype=torch.int64, device=local_sizes.device)
+    counts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(counts, n, group=group)
+    counts = [int(c.item()) for c in counts]
+    m = max(counts) if counts else 0
+    buf = torch.zeros(m, dtype=torch.int64, device=local_sizes.device)
+    buf[: local_sizes.numel()] = local_sizes.to(torch.int64)
+    parts = [torch.zeros_like(buf) for _ in range(world)]
+    dist.all_gather(parts, buf, group=group)
+    return torch.cat([p[:c] for p, c in zip(parts, counts)])
+
+
+def compress_stream_sharded(data, rank, world, compress_fn, group=None):
+    """Compress one stream `data` (bytes) across `world` ranks.
+
+    compress_fn(list_of_fragments, total_len) -> list of compressed fragments (no headers).
+    Returns (header, local_fragments, global_offsets_of_local_fragments, total_compressed_len);
+    header + all ranks' fragments written at their offsets is the snappy stream of `data`."""
+    import torch
+    total = len(data)
+    offs, lens = fragment_bounds(total)
+    lo, hi = shard_range(len(offs), rank, world)
+    frags = [data[int(o): int(o) + int(l)] for o, l in zip(offs[lo:hi], lens[lo:hi])]
+    out = compress_fn(frags, total) if frags else []
+    local = torch.tensor([len(x) for x in out], dtype=torch.int64)
+    sizes = gather_sizes(local, group).numpy()
+    header = varint32(total)
+    starts = len(header) + np.concatenate([[0], np.cumsum(sizes)[:-1]]) if len(sizes) else np.zeros(0, np.int64)
+    return header, out, starts[lo:hi], int(len(header) + sizes.sum())
+
+
+def assemble(header, pieces_with_offsets, total_len):
+    """Concatenate (offset, bytes) pieces from all ranks behind the header."""
+    buf = bytearray(total_len)
+    buf[: len(header)] = header
+    for off, piece in pieces_with_offsets:
+        buf[int(off): int(off) + len(piece)] = piece
+    return bytes(buf)

@@ -83,6 +83,32 @@ def test_reference_mode_dictionary_streams(sm, oracle, gpu_available):
         assert sm.compress(raw) == oracle.compress(raw)
 
 
+def test_reference_mode_fragments_device(sm, oracle, gpu_available):
+    """Fragments of one stream (sharded-stream building block, dist.py): device output equals
+    Snappy.jl's block loop (no headers, Q2 table size from the total length)."""
+    import torch
+    raw = read_testfile("html_x_4") + read_testfile("urls.10K")[:70000]
+    total = len(raw)
+    offs = list(range(0, total, 65536))
+    lens = [min(65536, total - o) for o in offs]
+    dev = torch.device("cuda", 0)
+    d_in = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    d_len = torch.tensor(lens, dtype=torch.int32, device=dev)
+    slot = 76496
+    d_out = torch.empty(slot * len(offs), dtype=torch.uint8, device=dev)
+    d_ooff = torch.arange(len(offs), dtype=torch.int64, device=dev) * slot
+    d_olen = torch.zeros(len(offs), dtype=torch.int32, device=dev)
+    sm.compress_fragments_device(d_in, d_off, d_len, d_out, d_ooff, d_olen, total, mode="reference")
+    torch.cuda.synchronize()
+    out = d_out.cpu().numpy()
+    ol = d_olen.cpu().numpy()
+    frags = [out[i * slot: i * slot + int(ol[i])].tobytes() for i in range(len(offs))]
+    for i, (o, l) in enumerate(zip(offs, lens)):
+        assert frags[i] == oracle.compress_fragment(raw[o:o + l], total)
+    assert oracle.encode32(total) + b"".join(frags) == oracle.compress(raw)
+
+
 # ---- fast mode --------------------------------------------------------------------------
 
 @pytest.mark.parametrize("fname", ROUNDTRIP_FILES)

@@ -12,6 +12,6 @@ for P in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_WR SQ_
          "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc $P -d "$OUT/p$i" -o pass -- \
-    python3 tools/kbench.py --op "$OP" --blocks 2000 --reps 3 --data "$DATA" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
+    python3 tools/kbench.py --op "$OP" --blocks ${BLOCKS:-2000} --reps 3 --data "$DATA" > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/p$i.log"; exit 1; }
 done
 echo done
