@@ -1,0 +1,46 @@
+"""Turn the PMC passes of tools/pmc_run.sh into profiles/<round>_pmc.json (bench.py's `traffic`).
+
+Usage: python tools/pmc_json.py <round-dir> <out.json>
+  <round-dir>/pmc_compress and <round-dir>/pmc_uncompress hold the rocprofv3 --pmc passes.
+
+HBM bytes per launch follow /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section):
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half of the bytes of a
+wide coalesced streaming read, so it is doubled.  Calibration on our own access pattern: the
+fast compressor reads every input byte exactly once with 16 B/lane loads, and 2 x FETCH_SIZE
+matches the algorithmic input bytes to within 1% (profiles/r01_pmc.json, "calibration").
+The decoder's copy-source re-reads are 8 B/lane and stay uncalibrated (noted per kernel).
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import summarise  # noqa: E402
+
+KERNELS = {"compress_fast": ("pmc_compress", "k_compress_fast"),
+           "uncompress": ("pmc_uncompress", "k_decompress")}
+
+
+def main(root, out_path):
+    res = {"source": "rocprofv3 --kernel-trace --pmc, one pass per counter group (tools/pmc_run.sh)",
+           "units": "bytes per launch (10000 x 64 KiB text blocks)"}
+    for key, (sub, kname) in KERNELS.items():
+        d = summarise(os.path.join(root, sub), kname)
+        if not d:
+            continue
+        ctr = next(iter(d.values()))
+        fetch = ctr.get("FETCH_SIZE", 0.0) * 1024.0
+        write = ctr.get("WRITE_SIZE", 0.0) * 1024.0
+        res[key] = {
+            "kernel": next(iter(d.keys()))[:60],
+            "fetch_size_bytes_raw": fetch,
+            "write_size_bytes": write,
+            "hbm_bytes_per_launch": 2.0 * fetch + write,
+            "counters": {k: v for k, v in sorted(ctr.items())},
+        }
+    json.dump(res, open(out_path, "w"), indent=1)
+    print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in res.items() if isinstance(v, dict)}))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
