@@ -4,11 +4,12 @@
 // uncompress, src/internal.jl:411-466) with a wave-parallel parse instead of the reference's
 // serial greedy loop (internal.jl:127-250).
 //
-// One workgroup of 8 waves per block; the block is staged once in LDS (64 KiB) beside a
-// shared 16 K-entry latest-position table (u32, 64 KiB) and a 256-entry private table per
-// wave (8 KiB): 136 KiB, one block per CU.  The block is cut into 128-byte chunks whose parse
-// never crosses the chunk end (copies are truncated there, literal runs end there), so the
-// chunks of a round are parsed independently: in round r wave w owns chunk 8r+w, two
+// One workgroup of W = 16 waves per block (four per SIMD, to hide the chain of LDS round
+// trips); the block is staged once in LDS (64 KiB) beside a shared 16 K-entry latest-position
+// table (u32, 64 KiB), a 256-entry private table per wave (16 KiB) and 5-level parse jump
+// tables (10 KiB): 154 KiB, one block per CU.  The block is cut into 128-byte chunks whose
+// parse never crosses the chunk end (copies are truncated there, literal runs end there), so
+// the chunks of a round are parsed independently: in round r wave w owns chunk W*r+w, two
 // positions per lane (q = c0 + 64*j + lane).  Per chunk:
 //  1. (a) insert every position into the shared table with ds_max_u32 (order-independent ->
 //     deterministic) and into the wave's private table with ds_max_rtn_u32, whose return is
@@ -18,9 +19,9 @@
 //     table after the round (if it is an earlier position); B = the shared table as of the
 //     previous round.  Both verified (4 bytes) and extended 16 bytes branch-free with unaligned
 //     ds_read_b64; the longer one wins;
-//  3. greedy walk over the two match ballots in SALU (s_ff1 + one v_readlane per copy);
-//     tokens land in lanes; sizes in closed form, DPP wave scan, chunk sizes exchanged
-//     through LDS -> exact output offsets;
+//  3. greedy parse by pointer doubling over the chunk (J_k = J_{k-1} o J_{k-1}, binary
+//     descent); the visited copies are compacted into token lanes; sizes in closed form,
+//     DPP wave scan, chunk sizes exchanged through LDS -> exact output offsets;
 //  4. (c) token lanes write tag bytes; position lanes scatter literal bytes.
 // Two barriers per round.  Output is deterministic (no order-dependent table state).
 #include "sm_device.h"
@@ -37,16 +38,17 @@ constexpr uint32_t kFTab = 1u << kFTabBits;   // shared table entries
 constexpr uint32_t kPrivBits = 8;
 constexpr uint32_t kPriv = 1u << kPrivBits;   // private (intra-chunk) table entries per wave
 constexpr uint32_t kChunk = 128;
-constexpr uint32_t kWavesPerBlock = 8;
+#ifndef SM_FAST_WAVES
+#define SM_FAST_WAVES 16
+#endif
+constexpr uint32_t kWavesPerBlock = SM_FAST_WAVES;  // 16: four waves per SIMD hide the LDS latency chain
 constexpr uint32_t kThreads = 64 * kWavesPerBlock;
-constexpr uint32_t kEager = 16;               // bytes compared past the first 4 before the wave takes over
-
-typedef uint16_t __attribute__((aligned(1))) fu16u;
-typedef uint32_t __attribute__((aligned(1))) fu32u;
-typedef uint64_t __attribute__((aligned(1))) fu64u;
-
-__device__ inline uint32_t ld32u(const uint8_t* p) { return *reinterpret_cast<const fu32u*>(p); }
-__device__ inline uint64_t ld64u(const uint8_t* p) { return *reinterpret_cast<const fu64u*>(p); }
+constexpr uint32_t kLevels = 5;              // J0..J4: the copy-to-copy walk of a chunk takes <= 31 steps
+constexpr uint32_t kEager = 16;               // bytes compared per candidate before the long-match loop
+#ifndef SM_FAST_NBR
+#define SM_FAST_NBR 4
+#endif
+constexpr uint32_t kNbr = SM_FAST_NBR;       // earlier chunks of the round probed for candidate C
 
 // emit_copy! byte count (internal.jl:306-329), closed form
 __device__ inline uint32_t copy_bytes_cf(uint32_t off, uint32_t L) {
@@ -84,39 +86,7 @@ __device__ inline void put_copy_cf(uint8_t* dst, uint32_t o, uint32_t off, uint3
   }
 }
 
-// match length of lds[i1..] vs lds[i2..] capped at avail, whole wave (512 B per round)
-__device__ inline uint32_t wave_match_len8(const uint8_t* lds, uint32_t i1, uint32_t i2, uint32_t avail,
-                                           uint32_t lane) {
-  uint32_t base = 0;
-  for (;;) {
-    uint32_t off = base + 8 * lane;
-    uint32_t res;
-    bool stop;
-    if (off >= avail) {
-      res = avail;
-      stop = true;
-    } else {
-      uint64_t x = ld64u(lds + i1 + off) ^ ld64u(lds + i2 + off);
-      uint32_t fb = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
-      res = min(off + fb, avail);
-      stop = (fb < 8) || (off + 8 >= avail);
-    }
-    uint64_t m = ballot(stop);
-    if (m) return readlane(res, ctz64(m));
-    base += 8 * kWave;
-  }
-}
-
-// bytes matching past the first 4 (0..kEager), branch-free
-__device__ inline uint32_t ext16(const uint8_t* d, uint32_t c, uint32_t q) {
-  uint64_t x0 = ld64u(d + c + 4) ^ ld64u(d + q + 4);
-  uint64_t x1 = ld64u(d + c + 12) ^ ld64u(d + q + 12);
-  uint32_t e0 = (uint32_t)(__builtin_ctzll(x0 | (1ull << 63)) >> 3);  // 0..7, or 7 if equal
-  uint32_t e1 = (uint32_t)(__builtin_ctzll(x1 | (1ull << 63)) >> 3);
-  return x0 ? e0 : (x1 ? 8 + e1 : 16);
-}
-
-__global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
+__global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* data = smem;                                                       // 64 KiB block
   uint32_t* T = reinterpret_cast<uint32_t*>(smem + kBlockSize);               // shared table
@@ -125,7 +95,7 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
   const uint32_t lane = tid & 63;
   uint32_t* P = T + kFTab + wave * kPriv;                                     // private table
   uint32_t* csize = T + kFTab + kWavesPerBlock * kPriv;                       // per-wave chunk sizes
-  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + kWavesPerBlock) + wave * 8 * kChunk;  // parse jump tables
+  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + kWavesPerBlock) + wave * kLevels * kChunk;  // parse jump tables
 
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.in_len[b];
@@ -136,17 +106,18 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
     return;
   }
 
-  // stage the block: 8 x 16 B per thread in flight when aligned
+  // stage the block: all 16 B loads of a thread in flight when aligned
   if (((uintptr_t)src & 15) == 0) {
     const uint4* s16 = reinterpret_cast<const uint4*>(src);
     uint4* d16 = reinterpret_cast<uint4*>(data);
     const uint32_t n16 = n >> 4;
     if (n16 == kBlockSize / 16) {
-      uint4 v[8];
+      constexpr int kStage = kBlockSize / 16 / kThreads;
+      uint4 v[kStage];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = s16[tid + i * kThreads];
+      for (int i = 0; i < kStage; ++i) v[i] = s16[tid + i * kThreads];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) d16[tid + i * kThreads] = v[i];
+      for (int i = 0; i < kStage; ++i) d16[tid + i * kThreads] = v[i];
     } else {
       for (uint32_t k = tid; k < n16; k += kThreads) d16[k] = s16[k];
       for (uint32_t k = (n & ~15u) + tid; k < n; k += kThreads) data[k] = src[k];
@@ -170,13 +141,14 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
   const uint32_t nchunks = (n + kChunk - 1) / kChunk;
   const uint32_t rounds = (nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
 
-  uint32_t w[2], t1[2];
+  uint64_t w[2];  // the 8 bytes at each position
+  uint32_t t1[2];
   {
     const uint32_t c0 = wave * kChunk;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       uint32_t q = c0 + 64 * j + lane;
-      w[j] = ld32u(data + (q < n ? q : 0));
+      w[j] = lds_ld64(data, q < n ? q : 0);
       t1[j] = 0;
     }
   }
@@ -193,7 +165,7 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t q = c0 + 64 * j + lane;
-        const uint32_t hm = w[j] * kHashMul;
+        const uint32_t hm = (uint32_t)w[j] * kHashMul;
         if (q + 4 <= n) {
           __hip_atomic_fetch_max(&T[hm >> (32 - kFTabBits)], q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           pin[j] = __hip_atomic_fetch_max(&P[hm >> (32 - kPrivBits)], q + 1, __ATOMIC_RELAXED,
@@ -207,33 +179,73 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
     uint32_t ta = 0, tb = 0, ntok = 0, incl = 0, sz = 0, litlen = 0, littag = 0, ls = 0;
     uint64_t ts0 = 0, ts1 = 0;
     if (active) {
+      // Candidates per position: A = the latest earlier position of the chunk with the same
+      // 8-bit hash (ds_max_rtn above), B = the shared table as of the previous round, C = the
+      // nearest earlier chunk of this round (waves wave-1..wave-kNbr) whose private table holds
+      // a 4-byte match (the positions the round-lagged shared table misses).  The longest
+      // match wins (ties: A, B, C).
       uint32_t Ls[2], offs[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t q = c0 + 64 * j + lane;
         const bool can = q + 4 <= ce;
-        const uint32_t cap = can ? ce - q - 4 : 0;
-        const uint32_t t2 = T[(w[j] * kHashMul) >> (32 - kFTabBits)];
-        uint32_t ca = pin[j] > c0 ? pin[j] - 1 : ((t2 != 0 && t2 - 1 < q) ? t2 - 1 : q);
-        uint32_t cb = t1[j] != 0 ? t1[j] - 1 : q;
-        const bool oka = can && ca < q && ld32u(data + ca) == w[j];
-        const bool okb = can && cb < q && cb != ca && ld32u(data + cb) == w[j];
-        const uint32_t la = oka ? 4 + min(ext16(data, ca, q), cap) : 0;
-        const uint32_t lb = okb ? 4 + min(ext16(data, cb, q), cap) : 0;
-        const bool useb = lb > la;
-        Ls[j] = (SM_ABLATE & 2) ? 0u : (useb ? lb : la);
-        offs[j] = q - (useb ? cb : ca);
+        const uint64_t wq = w[j];
+        const uint32_t ca = pin[j] > c0 ? pin[j] - 1 : q;
+        const uint32_t cb = t1[j] != 0 ? t1[j] - 1 : q;
+        uint32_t cc = q;
+        if (kNbr) {
+          const uint32_t h8 = ((uint32_t)wq * kHashMul) >> (32 - kPrivBits);
+          uint32_t v[kNbr ? kNbr : 1];
+#pragma unroll
+          for (uint32_t m = 1; m <= kNbr; ++m) v[m - 1] = m <= wave ? P[h8 - m * kPriv] : 0u;
+#pragma unroll
+          for (int m = (int)kNbr; m >= 1; --m)
+            cc = (v[m - 1] != 0 && lds_ld32(data, v[m - 1] - 1) == (uint32_t)wq) ? v[m - 1] - 1 : cc;
+        }
+        // verify 4 bytes, then grow to 8 and 16; every read is masked to the lanes still
+        // matching (an LDS access costs by its active lanes)
+        const uint32_t cand[3] = {ca, cb, cc};
+        uint32_t len[3];
+        len[0] = (can && ca < q && lds_ld32(data, ca) == (uint32_t)wq) ? 4u : 0u;
+        len[1] = (can && cb < q && cb != ca && lds_ld32(data, cb) == (uint32_t)wq) ? 4u : 0u;
+        len[2] = (can && cc < q && cc != ca && cc != cb) ? 4u : 0u;  // verified by the probe
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          if (len[i]) {
+            const uint32_t x = lds_ld32(data, cand[i] + 4) ^ (uint32_t)(wq >> 32);
+            len[i] = x ? 4 + ((uint32_t)__builtin_ctz(x) >> 3) : 8u;
+          }
+        }
+        if (len[0] == 8 || len[1] == 8 || len[2] == 8) {
+          const uint64_t wq2 = lds_ld64(data, q + 8);
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            if (len[i] == 8) {
+              const uint64_t x = lds_ld64(data, cand[i] + 8) ^ wq2;
+              len[i] = x ? 8 + (uint32_t)(__builtin_ctzll(x) >> 3) : 16u;
+            }
+          }
+        }
+        uint32_t L = len[0], c = ca;
+#pragma unroll
+        for (int i = 1; i < 3; ++i) {
+          c = len[i] > L ? cand[i] : c;
+          L = len[i] > L ? len[i] : L;
+        }
+        L = min(L, ce - q);
+        Ls[j] = (SM_ABLATE & 2) ? 0u : L;
+        offs[j] = q - c;
       }
       // finish matches that filled the eager window: 8 bytes per lane per step
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t q = c0 + 64 * j + lane;
         uint32_t L = Ls[j];
-        bool more = L >= 4 + kEager && q + L < ce;
+        bool more = L >= kEager && q + L < ce;
         while (ballot(more)) {
           if (more) {
             const uint32_t avail = ce - q - L;
-            const uint64_t x = ld64u(data + q - offs[j] + L) ^ ld64u(data + q + L);
+            const uint64_t x = lds_ld64(data, q - offs[j] + L) ^ lds_ld64(data, q + L);
             const uint32_t fb = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
             L += min(fb, avail);
             more = fb == 8 && avail > 8;
@@ -241,21 +253,28 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
         }
         Ls[j] = L;
       }
-      // Greedy parse by pointer doubling (no serial loop): J0[r] = r + max(L(r), 1) over the
-      // chunk's 128 positions, J_k = J_{k-1} o J_{k-1}; position r is visited by the greedy
-      // walk from 0 iff the binary descent along J_7..J_0 (largest visited position <= r)
-      // lands on r.  Visited match positions are the copies.
+      // Greedy parse by pointer doubling (no serial loop) over the chunk's 128 positions.
+      // J0 skips literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a
+      // non-match), else the chunk end, so the greedy walk from 0 steps only between copies
+      // (<= 32 copies of >= 4 bytes: 31 steps); J_k = J_{k-1} o J_{k-1}.  Position r is
+      // visited iff the binary descent along J_4..J_0 (largest visited position <= r) lands
+      // on r; visited match positions are the copies.
       uint32_t cur[2] = {0xffffu, 0xffffu};  // no copies at all (incompressible): skip the parse
-      if (ballot(Ls[0] != 0 || Ls[1] != 0)) {
+      const uint64_t M0 = ballot(Ls[0] != 0), M1 = ballot(Ls[1] != 0);
+      if (M0 | M1) {
         uint32_t jv[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           const uint32_t r = 64 * j + lane;
-          jv[j] = r + max(Ls[j], 1u);  // <= 255
+          const uint32_t x = r + Ls[j];  // <= 128: copies end inside the chunk
+          const uint64_t m0 = x < 64 ? M0 >> x : 0;
+          const uint64_t m1 = x < 64 ? M1 : (x < 128 ? M1 >> (x - 64) : 0);
+          const uint32_t b1 = x < 64 ? 64u : x;
+          jv[j] = m0 ? x + (uint32_t)__builtin_ctzll(m0) : (m1 ? b1 + (uint32_t)__builtin_ctzll(m1) : kChunk);
           jt[r] = (uint8_t)jv[j];
         }
 #pragma unroll
-        for (int k = 1; k < 8; ++k) {
+        for (int k = 1; k < (int)kLevels; ++k) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             jv[j] = jv[j] < kChunk ? jt[(k - 1) * kChunk + jv[j]] : jv[j];
@@ -264,7 +283,7 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
         }
         cur[0] = cur[1] = 0;
 #pragma unroll
-        for (int k = 7; k >= 0; --k) {
+        for (int k = kLevels - 1; k >= 0; --k) {
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             const uint32_t t = jt[k * kChunk + cur[j]];
@@ -285,7 +304,7 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
         const uint32_t l = 63 - (uint32_t)__builtin_clzll(m);
         last_end = 64 * j + l + readlane(j ? Ls[1] : Ls[0], l);
       }
-      // compact the copies into lanes 0..nmatch-1 (slots reuse J level 0..3, no longer read)
+      // compact the copies into lanes 0..nmatch-1 (slots reuse J levels 0..4, no longer read)
       uint2* slots = reinterpret_cast<uint2*>(jt);
       if (tok0) slots[__builtin_amdgcn_mbcnt_hi((uint32_t)(ts0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ts0, 0u))] =
           make_uint2(lane | (Ls[0] << 16), offs[0]);
@@ -319,15 +338,16 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
     }
 
     // next round: words and first-chance candidates (table as of this round)
-    uint32_t wn[2], t1n[2];
+    uint64_t wn[2];
+    uint32_t t1n[2];
     {
       const uint32_t k2 = k + kWavesPerBlock;
       const uint32_t c2 = k2 * kChunk;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t q = c2 + 64 * j + lane;
-        wn[j] = ld32u(data + (q < n ? q : 0));
-        t1n[j] = k2 < nchunks ? T[(wn[j] * kHashMul) >> (32 - kFTabBits)] : 0;
+        wn[j] = lds_ld64(data, q < n ? q : 0);
+        t1n[j] = k2 < nchunks ? T[((uint32_t)wn[j] * kHashMul) >> (32 - kFTabBits)] : 0;
       }
     }
     __syncthreads();  // B2
@@ -378,7 +398,9 @@ __global__ __launch_bounds__(512) void k_compress_fast(CompressArgs a) {
 }
 
 constexpr size_t kFastLds =
-    kBlockSize + 4 * (kFTab + kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * 8 * kChunk;
+    kBlockSize + 4 * (kFTab + kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * kLevels * kChunk;
+static_assert(kFastLds <= 160 * 1024, "fast compressor LDS exceeds a CU");
+static_assert(65 * sizeof(uint2) <= kLevels * kChunk, "token slots overflow the jump tables");
 
 hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s) {
   static bool attr_set = false;

@@ -164,9 +164,8 @@ __device__ inline void ring_put(uint8_t* ring, uint32_t base, uint32_t word, uin
   if (r == 0 && lane < 4) reinterpret_cast<uint32_t*>(ring + kRing)[lane] = word;  // mirror
 }
 
-__device__ inline uint64_t ring_get8(const uint8_t* ring, uint32_t pos) {
-  return *reinterpret_cast<const du64u*>(ring + (pos & (kRing - 1)));
-}
+// 8 stream bytes at pos (aligned dword reads: the mirror covers the 12 bytes past kRing)
+__device__ inline uint64_t ring_get8(const uint8_t* ring, uint32_t pos) { return lds_ld64(ring, pos & (kRing - 1)); }
 
 __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t size,
                                        uint8_t* out, uint8_t* ring, uint16_t* jt, uint32_t lane) {

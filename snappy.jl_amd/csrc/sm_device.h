@@ -97,12 +97,22 @@ __device__ inline uint32_t scan_dpp(uint32_t v) {
   return v;
 }
 
-// unaligned little-endian 32-bit load from an LDS byte array (two aligned dword reads +
-// v_alignbyte_b32).  The array must have >= 4 readable bytes past pos+3.
+// Unaligned little-endian loads from an LDS byte array, built from aligned dword reads +
+// v_alignbyte_b32.  A misaligned ds_read_b32/b64 is serviced one lane per LDS cycle (~64
+// cycles per wave-instruction) against 2-8 aligned and ~15 for this form on random
+// addresses (tools/lds_bench.hip, measured on MI355X).
+// lds_ld32: the array must have >= 4 readable bytes past pos+3.
 __device__ inline uint32_t lds_ld32(const uint8_t* lds, uint32_t pos) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (pos & ~3u));
   uint32_t lo = w[0], hi = w[1];
   return __builtin_amdgcn_alignbyte(hi, lo, pos & 3u);
+}
+
+// lds_ld64: >= 4 readable bytes past pos+7.
+__device__ inline uint64_t lds_ld64(const uint8_t* lds, uint32_t pos) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (pos & ~3u));
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = pos & 3u;
+  return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
 __device__ inline uint32_t hash32(uint32_t bytes, uint32_t shift) { return (bytes * kHashMul) >> shift; }

@@ -20,6 +20,8 @@ static uint32_t copy_bytes(uint32_t off, uint32_t len) {
 
 // policy: 0 = first-chance only (prior rounds), 1 = second chance else first, 2 = best of both,
 //         3 = exact latest-earlier (ideal table)
+static int g_nbr = 0, g_first = 0, g_skip = 0;  // probe the private tables of g_nbr previous chunks
+
 static uint64_t model_block(const uint8_t* d, uint32_t n, uint32_t chunk, uint32_t waves, uint32_t tab,
                             int policy, int exact_intrachunk) {
   uint32_t* T = calloc(tab, 4);
@@ -40,6 +42,13 @@ static uint64_t model_block(const uint8_t* d, uint32_t n, uint32_t chunk, uint32
       cand2[q] = cq;
       T[h] = q + 1;
     }
+    // private tables (8-bit hash) of the round's chunks: max position per bucket
+    uint32_t P[64][256];
+    for (uint32_t k = r * waves; k < (r + 1) * waves && k < nch; ++k) {
+      uint32_t c0 = k * chunk, ce = c0 + chunk < n ? c0 + chunk : n;
+      memset(P[k - r * waves], 0, sizeof(P[0]));
+      for (uint32_t q = c0; q + 4 <= n && q < ce; ++q) P[k - r * waves][(ld32(d + q) * 0x1e35a7bdu) >> 24] = q + 1;
+    }
     // second-chance table = max after round (T now)
     for (uint32_t k = r * waves; k < (r + 1) * waves && k < nch; ++k) {
       uint32_t c0 = k * chunk, ce = c0 + chunk < n ? c0 + chunk : n;
@@ -57,9 +66,19 @@ static uint64_t model_block(const uint8_t* d, uint32_t n, uint32_t chunk, uint32
             if (policy == 0 || policy == 2 || nc == 0) cands[nc++] = cand1[p];
             if (exact_intrachunk && exact && exact - 1 >= c0) cands[nc++] = exact;
           }
-          for (int i = 0; i < nc; ++i) {
-            if (!cands[i]) continue;
-            uint32_t c = cands[i] - 1;
+          uint32_t nb[64]; int nn = 0, have = 0;
+          for (int i = 0; i < nc; ++i)
+            if (cands[i] && cands[i] - 1 < p && ld32(d + cands[i] - 1) == ld32(d + p)) have = 1;
+          for (int m = 1; m <= g_nbr && !(g_skip && have) && (int)(k - r * waves) - m >= 0; ++m) {
+            uint32_t v = P[k - r * waves - m][(ld32(d + p) * 0x1e35a7bdu) >> 24];
+            if (g_first && !(v && v - 1 < p && ld32(d + v - 1) == ld32(d + p))) continue;
+            nb[nn++] = v;
+            if (g_first) break;
+          }
+          for (int i = 0; i < nc + nn; ++i) {
+            uint32_t cv = i < nc ? cands[i] : nb[i - nc];
+            if (!cv) continue;
+            uint32_t c = cv - 1;
             if (c >= p) continue;
             uint32_t L = 0;
             while (p + L < ce && d[c + L] == d[p + L]) ++L;
@@ -86,10 +105,15 @@ int main(int argc, char** argv) {
     total += fread(buf + total, 1, cap - total, f);
     fclose(f);
   }
+  if (getenv("NBR")) g_nbr = atoi(getenv("NBR"));  // e.g. NBR=4 FIRST=1 (nearest verified only)
+  if (getenv("FIRST")) g_first = 1;
+  if (getenv("SKIP")) g_skip = 1;                   // probe only positions without a verified A/B
   struct { uint32_t chunk, waves, tab; int pol, intra; } cfg[] = {
       {256, 4, 16384, 2, 1}, {256, 8, 16384, 2, 1}, {128, 8, 16384, 2, 1}, {256, 8, 16384, 1, 1},
       {256, 4, 12288, 2, 1}, {256, 8, 12288, 2, 1}, {256, 4, 8192, 2, 1}, {256, 8, 8192, 2, 1},
       {512, 8, 16384, 2, 1}, {256, 16, 16384, 2, 1}, {256, 8, 16384, 0, 1},
+      {128, 16, 16384, 2, 1}, {64, 16, 16384, 2, 1}, {64, 32, 16384, 2, 1}, {128, 8, 16384, 3, 1},
+      {128, 16, 16384, 0, 1}, {128, 16, 16384, 1, 1}, {128, 16, 16384, 0, 0}, {128, 16, 16384, 2, 0},
   };
   for (size_t c = 0; c < sizeof(cfg) / sizeof(cfg[0]); ++c) {
     uint64_t out = 0, in = 0;

@@ -44,8 +44,9 @@ def main():
     nbytes = args.blocks * bench.BLOCK
     print("%s %s: %.3f ms/launch, %.2f GB/s (uncompressed bytes), ratio %.4f" % (
         args.op, args.data, dt * 1e3, nbytes / dt / 1e9, float(b.comp_len.sum()) / nbytes))
-    if args.op == "uncompress":
-        print("roundtrip ok:", b.verify())
+    if args.op != "uncompress":
+        b.uncompress(sm)
+    print("roundtrip ok:", b.verify())
 
 
 if __name__ == "__main__":
