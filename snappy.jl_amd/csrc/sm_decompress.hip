@@ -43,6 +43,8 @@ typedef uint32_t __attribute__((aligned(1))) du32u;
 typedef uint64_t __attribute__((aligned(1))) du64u;
 
 constexpr uint32_t kRing = 1024;
+constexpr int kWalkLevels = 6;  // J0..J5: 63 steps = the 64 tags of a batch
+constexpr int kPass = 2;        // 8-byte chunks per execution pass (most tags are <= 16 B)
 
 __device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
   if (p + 3 < N && (((uintptr_t)(in + p)) & 3) == 0) return *reinterpret_cast<const uint32_t*>(in + p);
@@ -206,9 +208,10 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     // Parallel tag walk by pointer doubling over the 256 window positions (VALU + LDS, no
     // serial SALU loop).  J0[p] = p + size(p); a position whose tag is a long literal, or that
     // lies at/after the parse limit (window end or N-1, internal.jl:416), is a stop node
-    // (J0[p] = p, self-loop).  J_k = J_{k-1} o J_{k-1} (k < 8; sizes >= 2 so a window holds
-    // <= 128 tags).  Position p is a tag start iff the binary descent from the window's first
-    // tag s0 along J_7..J_0 (largest chain element <= p) lands on p.
+    // (J0[p] = p, self-loop).  J_k = J_{k-1} o J_{k-1}, k < kWalkLevels: a batch takes at most
+    // 64 tags, i.e. chain elements 0..63 steps from the window's first tag s0, and the binary
+    // descent from s0 along J_5..J_0 (largest chain element <= p within 63 steps) lands on p
+    // iff p is one of them.
     const uint32_t wlim = (int64_t)(wb + 256) < Nm1 ? wb + 256 : (uint32_t)Nm1;
     const uint32_t rlim = wlim - wb;
     const uint32_t s0 = ip - wb;
@@ -225,7 +228,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     uint16_t* jt0 = jt;
     *reinterpret_cast<uint2*>(jt0 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
 #pragma unroll
-    for (int k = 1; k < 8; ++k) {
+    for (int k = 1; k < kWalkLevels; ++k) {
       const uint16_t* prev = jt + (k - 1) * 256;
 #pragma unroll
       for (int j = 0; j < 4; ++j) J[j] = J[j] < 256 ? prev[J[j]] : J[j];
@@ -233,7 +236,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     }
     uint32_t cur[4] = {s0, s0, s0, s0};
 #pragma unroll
-    for (int k = 7; k >= 0; --k) {
+    for (int k = kWalkLevels - 1; k >= 0; --k) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const uint32_t t = jt[k * 256 + cur[j]];
@@ -333,7 +336,9 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         if (k < L) store_partial(out, o + k, ring_get8(ring, s + k), L - k);
       }
 
-      // Dependency rounds.  Every tag of a round issues all its loads before any store:
+      // Dependency rounds.  A round's stores never touch bytes another ready tag of the round
+      // reads (a source overlapping this round's output makes its tag wait), so each pass of
+      // kPass chunks issues its loads, then its stores:
       //  * literal (<= 64 B): 8-byte pieces of the LDS ring;
       //  * copy: its source window S = out[slo, slo+offset) is final when the round starts, and
       //    output byte j is S[j mod offset] (incremental_copy_slow!, internal.jl:477-481), so
@@ -347,14 +352,14 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
                            ((SM_ABLATE_D & 2) || !iscopy || shi <= O0 || ((~done) & range) == 0);
         const uint64_t rm = ballot(ready);
         const uint32_t L = iscopy ? len : litlen;
-        for (uint32_t base = 0; base < 64; base += 32) {
+        for (uint32_t base = 0; base < 64; base += 8 * kPass) {
           const bool act = ready && L > base;
           if (!ballot(act)) break;
           if (act) {
-            uint64_t v[4];
+            uint64_t v[kPass];
             if (!iscopy) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i)
+              for (int i = 0; i < kPass; ++i)
                 v[i] = base + 8 * i < L ? ring_get8(ring, lsrc + base + 8 * i) : 0ull;
             } else if (offset >= 8) {
               const uint64_t B = *reinterpret_cast<const du64u*>(out + slo);
@@ -362,14 +367,14 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
               while (m0 >= offset) m0 -= offset;
               uint32_t m = m0;
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
+              for (int i = 0; i < kPass; ++i) {
                 v[i] = base + 8 * i < L ? *reinterpret_cast<const du64u*>(out + slo + m) : 0ull;
                 m += 8;
                 if (m >= offset) m -= offset;
               }
               m = m0;
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
+              for (int i = 0; i < kPass; ++i) {
                 const uint32_t keep = offset - m;  // bytes of this chunk before S wraps
                 if (keep < 8) v[i] = (v[i] & ((1ull << (8 * keep)) - 1)) | (B << (8 * keep));
                 m += 8;
@@ -388,14 +393,14 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
               uint32_t m = base;
               while (m >= offset) m -= offset;
 #pragma unroll
-              for (int i = 0; i < 4; ++i) {
+              for (int i = 0; i < kPass; ++i) {
                 v[i] = m ? ((p0 >> (8 * m)) | (p1 << (8 * (8 - m)))) : p0;
                 m += 8;
                 while (m >= offset) m -= offset;
               }
             }
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+            for (int i = 0; i < kPass; ++i)
               if (base + 8 * i < L) store_partial(out, opt + base + 8 * i, v[i], L - base - 8 * i);
           }
         }
@@ -459,7 +464,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
 
 __global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t sjt[8 * 256];  // tag-walk jump tables
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[kWalkLevels * 256];  // tag-walk jump tables
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
   const uint8_t* in = a.in + a.in_off[b];
