@@ -201,20 +201,20 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         issue_pre2 = false;
       }
     }
-    // speculative tag sizes for positions [wb, wb+256)
-    const uint64_t cw = ring_get8(ring, wb + 4 * lane);
+    // speculative tag sizes for the window [ip, ip+256) (inside the ring: ip < wb+256; a
+    // batch's literals end before ip+256+200 < wb+768)
+    const uint64_t cw = ring_get8(ring, ip + 4 * lane);
     const uint32_t sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
 
     // Parallel tag walk by pointer doubling over the 256 window positions (VALU + LDS, no
     // serial SALU loop).  J0[p] = p + size(p); a position whose tag is a long literal, or that
     // lies at/after the parse limit (window end or N-1, internal.jl:416), is a stop node
     // (J0[p] = p, self-loop).  J_k = J_{k-1} o J_{k-1}, k < kWalkLevels: a batch takes at most
-    // 64 tags, i.e. chain elements 0..63 steps from the window's first tag s0, and the binary
-    // descent from s0 along J_5..J_0 (largest chain element <= p within 63 steps) lands on p
-    // iff p is one of them.
-    const uint32_t wlim = (int64_t)(wb + 256) < Nm1 ? wb + 256 : (uint32_t)Nm1;
-    const uint32_t rlim = wlim - wb;
-    const uint32_t s0 = ip - wb;
+    // 64 tags, i.e. chain elements 0..63 steps from the window's first position (ip), and the
+    // binary descent from 0 along J_5..J_0 (largest chain element <= p within 63 steps) lands
+    // on p iff p is one of them.
+    const uint32_t wlim = (int64_t)(ip + 256) < Nm1 ? ip + 256 : (uint32_t)Nm1;
+    const uint32_t rlim = wlim - ip;
     uint32_t J[4], nxt[4];
     bool stopn[4];
 #pragma unroll
@@ -234,7 +234,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       for (int j = 0; j < 4; ++j) J[j] = J[j] < 256 ? prev[J[j]] : J[j];
       *reinterpret_cast<uint2*>(jt + k * 256 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
     }
-    uint32_t cur[4] = {s0, s0, s0, s0};
+    uint32_t cur[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int k = kWalkLevels - 1; k >= 0; --k) {
 #pragma unroll
@@ -248,7 +248,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t p = 4 * lane + j;
-      isv[j] = cur[j] == p && p >= s0 && !stopn[j];  // a tag of this batch
+      isv[j] = cur[j] == p && !stopn[j];  // a tag of this batch
       cnt += isv[j] ? 1u : 0u;
     }
     const uint32_t rank0 = scan_dpp(cnt) - cnt;
@@ -267,11 +267,11 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     bool big = false;
     if (ntok) {
       const uint32_t sv = reinterpret_cast<const uint32_t*>(jt)[lane < ntok ? lane : 0];
-      tpos = wb + (sv & 0xffff);
-      ipw = wb + readlane(sv >> 16, ntok - 1);
+      tpos = ip + (sv & 0xffff);
+      ipw = ip + readlane(sv >> 16, ntok - 1);
     }
     if (ipw < wlim) {
-      const uint32_t rel = ipw - wb;
+      const uint32_t rel = ipw - ip;
       big = ((readlane(sizes, rel >> 2) >> ((rel & 3) * 8)) & 0xff) == 255;
     }
 

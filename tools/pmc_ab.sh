@@ -14,6 +14,6 @@ for L in "$@"; do
     SNAPPY_MI355X_LIB=$L timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv --pmc $P -d "$OUT/$tag/p$i" -o pass -- \
       python3 tools/kbench.py --op "$OP" --blocks ${BLOCKS:-4000} --reps 2 --data "$DATA" > "$OUT/$tag/p$i.log" 2>&1 || { echo "pass $i failed"; tail -5 "$OUT/$tag/p$i.log"; exit 1; }
   done
-  python3 tools/pmc_summary.py $OUT/$tag k_compress > $OUT/$tag.txt
+  python3 tools/pmc_summary.py $OUT/$tag ${KF:-k_compress} > $OUT/$tag.txt
 done
 echo done
