@@ -50,6 +50,20 @@ constexpr uint32_t kEager = 16;               // bytes compared per candidate be
 #endif
 constexpr uint32_t kNbr = SM_FAST_NBR;       // earlier chunks of the round probed for candidate C
 
+// literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
+__device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
+
+// literal tag of `ts` bytes (lit_tag_bytes(len)) for a run of len bytes at dst[o]
+__device__ inline void put_lit_tag(uint8_t* dst, uint32_t o, uint32_t ts, uint32_t len) {
+  if (ts == 1) {
+    dst[o] = (uint8_t)((len - 1) << 2);
+  } else if (ts >= 2) {
+    dst[o] = (uint8_t)((58 + ts) << 2);  // 60: one length byte, 61: two
+    dst[o + 1] = (uint8_t)(len - 1);
+    if (ts == 3) dst[o + 2] = (uint8_t)((len - 1) >> 8);
+  }
+}
+
 // emit_copy! byte count (internal.jl:306-329), closed form
 __device__ inline uint32_t copy_bytes_cf(uint32_t off, uint32_t L) {
   uint32_t k = L >= 68 ? ((L - 68) >> 6) + 1 : 0;
@@ -328,11 +342,15 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       ls = lane == 0 ? c0 : prev_end;
       if (lane < ntok) {
         litlen = tq - ls;
-        littag = litlen == 0 ? 0 : (litlen <= 60 ? 1 : 2);
+        littag = lit_tag_bytes(litlen);
         sz = littag + litlen + (tL ? copy_bytes_cf(tb, tL) : 0);
       }
       incl = scan_dpp(sz);
-      if (lane == 0) csize[wave] = readlane(incl, ntok - 1);
+      // chunk info for the round layout: unmerged size | leading literal piece | trailing
+      // literal piece | no copies at all
+      const uint32_t trail = ce - c0 - last_end;
+      if (lane == 0)
+        csize[wave] = readlane(incl, ntok - 1) | (readlane(litlen, 0) << 11) | (trail << 19) | ((nmatch == 0) << 27);
     } else {
       if (lane == 0) csize[wave] = 0;
     }
@@ -352,27 +370,59 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     }
     __syncthreads();  // B2
 
-    // (c) emit at the exact output offset
-    uint32_t before = 0, total = 0;
+    // (c) round layout, lane-parallel over the round's chunks (lane u = chunk u): a literal
+    // run that crosses chunk boundaries inside the round is emitted once, with one tag for
+    // its total length in the chunk where it starts (runs restart at round boundaries).
+    //   cont_in[u]: chunk u's leading literal piece continues chunk u-1's trailing piece (no tag)
+    //   mid[u]:     chunk u is all literal and continues a run (no tag of its own)
+    //   start[u]:   chunk u's trailing piece starts a run; if cont_in[u+1] the run spans chunks
+    //               and its tag encodes the run length up to the end of the last piece.
+    uint32_t myb, mycont, myrun, total;
+    {
+      const uint32_t info = lane < kWavesPerBlock ? csize[lane] : 0u;
+      const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0xffu, trl = (info >> 19) & 0xffu;
+      const bool nocp = (info >> 27) & 1u;
+      const uint32_t trl_prev = __shfl_up(trl, 1, 64);
+      const bool cont_in = lane > 0 && lane < kWavesPerBlock && trl_prev > 0 && lead > 0;
+      const bool mid = nocp && cont_in;
+      const bool start = trl > 0 && !mid;
+      const bool cont_next = __shfl_down((uint32_t)cont_in, 1, 64) != 0 && lane + 1 < kWavesPerBlock;
+      const uint32_t cu = (r * kWavesPerBlock + lane) * kChunk;              // chunk start
+      const uint32_t ceu = min(cu + kChunk, n);
+      // the run ending in chunk u ends at cu + lead; a run starting in chunk v ends in the
+      // first later chunk whose piece ends it (suffix min over lanes)
+      const bool ends = cont_in && !(mid && cont_next);
+      uint32_t nxt = ends ? lane : 0xffu;
 #pragma unroll
-    for (uint32_t v = 0; v < kWavesPerBlock; ++v) {
-      const uint32_t s = csize[v];
-      before += v < wave ? s : 0;
-      total += s;
+      for (uint32_t d = 1; d < kWavesPerBlock; d <<= 1) {
+        const uint32_t o2 = __shfl_down(nxt, d, 64);
+        nxt = (lane + d < kWavesPerBlock && o2 < nxt) ? o2 : nxt;
+      }
+      nxt = __shfl_down(nxt, 1, 64);                                         // first end after u
+      const uint32_t endpos = __shfl(cu + lead, nxt & 63u, 64);
+      const uint32_t runlen = (start && cont_next) ? endpos - (ceu - trl) : 0u;
+      const uint32_t Sm = S - (cont_in ? lit_tag_bytes(lead) : 0u) +
+                          (runlen ? lit_tag_bytes(runlen) - lit_tag_bytes(trl) : 0u);
+      const uint32_t inclm = scan_dpp(lane < kWavesPerBlock ? Sm : 0u);
+      total = readlane(inclm, kWavesPerBlock - 1);
+      myb = readlane(inclm - Sm, wave);
+      mycont = readlane((uint32_t)cont_in, wave);
+      myrun = readlane(runlen, wave);
     }
     if (active && !(SM_ABLATE & 1)) {
-      const uint32_t o = op + before + incl - sz;
+      const uint32_t rm = mycont ? readlane(littag, 0) : 0u;                 // leading tag removed
       const uint32_t tq = c0 + (ta & 0xffff), tL = ta >> 16;
-      if (lane < ntok) {
-        if (littag == 1) {
-          dst[o] = (uint8_t)((litlen - 1) << 2);
-        } else if (littag == 2) {
-          dst[o] = (uint8_t)(60 << 2);
-          dst[o + 1] = (uint8_t)(litlen - 1);
-        }
-        if (tL) put_copy_cf(dst, o + littag + litlen, tb, tL);
+      const uint32_t o = op + myb + incl - sz - (lane > 0 ? rm : 0u);
+      uint32_t mytag = (lane == 0 && mycont) ? 0u : littag, tagv = litlen;
+      if (myrun && lane == ntok - 1) {                                       // the run's trailing token
+        mytag = lit_tag_bytes(myrun);
+        tagv = myrun;
       }
-      const int32_t delta = (int32_t)(o + littag) - (int32_t)ls;
+      if (lane < ntok) {
+        put_lit_tag(dst, o, mytag, tagv);
+        if (tL) put_copy_cf(dst, o + mytag + litlen, tb, tL);
+      }
+      const int32_t delta = (int32_t)(o + mytag) - (int32_t)ls;
       const uint32_t end = tq + tL;
       uint32_t below = 0;
 #pragma unroll
