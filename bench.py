@@ -33,6 +33,7 @@ TEXTS = ["alice29.txt", "asyoulik.txt", "lcet10.txt", "plrabn12.txt"]
 BLOCK = 65536
 SLOT = 76496  # >= max_compressed_length(65536) = 76490, 16-B aligned
 HBM_PEAK_GBPS = 8000.0
+METRIC = "GB/s compressed+decompressed (batched blocks) at 1/2/4/8 GPUs; % HBM peak"  # BASELINE.json
 ROUND = "r01"
 
 
@@ -236,6 +237,11 @@ def main():
     if args.extras:
         t_ref = time_kernel(lambda: batch.compress(sm, "reference"), 1)
         extras["reference_mode_compress_GBps"] = round(in_bytes / (t_ref * 1e-3) / 1e9, 3)
+        # config 3 with the exact (Snappy.jl byte-identical) streams as input
+        t_rd3 = time_kernel(lambda: batch.uncompress(sm), 3)
+        ok = ok and batch.verify()
+        extras["reference_streams_uncompress_GBps"] = round(in_bytes / (t_rd3 * 1e-3) / 1e9, 3)
+        extras["reference_ratio"] = round(int(batch.comp_len.to(torch.int64).sum()) / in_bytes, 5)
         del batch
         torch.cuda.empty_cache()
         rb = Batch(random_blocks(args.blocks, 0x5EED + 1 + rank), dev)
@@ -256,7 +262,7 @@ def main():
     value = 2.0 * in_bytes * args.steps * world / elapsed / 1e9
     if rank == 0:
         line = {
-            "metric": "GB/s compressed+decompressed (batched 64 KiB blocks)",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GB/s",
             "n_gpus": world,
