@@ -76,10 +76,27 @@ __device__ inline uint32_t emit_copy_g(uint8_t* dst, uint32_t op, uint32_t offse
 __device__ inline uint32_t uld32(const uint8_t* lds, uint32_t pos) { return uniform(lds_ld32(lds, pos)); }
 
 // ---- reference mode ------------------------------------------------------------------
+//
+// Batched exact probes.  After every copy the reference's literal search probes positions
+// p0 + D[k], D[0] = 0, D[k+1] = D[k] + (skip_k >> 5), skip_0 = 32, skip_{k+1} = skip_k +
+// (skip_k >> 5) (internal.jl:162-175): a fixed sequence, so 64 probes go in one step, lane j =
+// probe k0 + j.  Probe k runs only if p0 + D[k+1] <= ip_limit (:175, checked before the probe).
+// Its candidate is the table entry as of just before it (:190), i.e. the latest earlier
+// insert with its hash.  Inserted positions only ever increase within a fragment (probes, then
+// ip-1 and ip after a copy, :228-235), so the table holds pos+1 (0 = never written, read as
+// candidate 0 exactly like the reference's 0xffff refill, Snappy.jl:30 / internal.jl:190) and
+// ds_max_rtn_u32 gives every lane its exact sequential candidate: conflicting lanes of one
+// instruction are serviced in ascending lane order on gfx950 (tools/probe_lds.hip; the
+// byte-parity tests pin it).  The first lane whose candidate matches is the reference's
+// match; the inserts of later lanes never happened sequentially and are undone exactly: for
+// each hash, the first later lane's return value is the entry's correct value.
+
+constexpr uint32_t kMaxProbes = 320;  // D[k] > 65536 for k >= ~250: a search never gets further
 
 __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sdata[kBlockSize + kLdsPad];
-  __shared__ __attribute__((aligned(16))) uint16_t stab[kMaxHashTableSize];
+  __shared__ __attribute__((aligned(16))) uint32_t stab[kMaxHashTableSize];  // pos + 1, 0 = empty
+  __shared__ uint32_t sD[kMaxProbes + 1];                                     // probe offsets
 
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
@@ -95,9 +112,15 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
   if (lane < kLdsPad) sdata[n + lane] = 0;
   const uint32_t tsize = a.table_size ? a.table_size : hashtable_size(n);      // Snappy.jl:27 (Q2)
   const uint32_t shift = 32 - (31 - __builtin_clz(tsize));                     // internal.jl:128
-  {
-    uint32_t* t32 = reinterpret_cast<uint32_t*>(stab);
-    for (uint32_t k = lane; k < tsize / 2; k += kWave) t32[k] = 0xffffffffu;   // Snappy.jl:30
+  for (uint32_t k = lane; k < tsize; k += kWave) stab[k] = 0;                  // Snappy.jl:30
+  if (lane == 0) {
+    uint32_t d = 0, skip = 32;
+    for (uint32_t k = 0; k <= kMaxProbes; ++k) {
+      sD[k] = d;
+      const uint32_t step = skip >> 5;                                         // :170-172
+      skip += step;
+      d = min(d + step, 0x20000u);
+    }
   }
   __syncthreads();
 
@@ -112,22 +135,32 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
 
   if (n >= kInputMarginBytes) {                                                // internal.jl:133
     for (;;) {
-      uint32_t skip = 32;                                                      // :162
       ip += 1;                                                                 // :163
-      uint32_t next_hash = hash32(uld32(sdata, ip), shift);
-      uint32_t next_ip = ip;
-      for (;;) {                                                               // :167-194
-        ip = next_ip;
-        uint32_t cur_hash = next_hash;
-        uint32_t step = skip >> 5;
-        skip += step;
-        next_ip = ip + step;
-        if ((int32_t)next_ip > ip_limit) goto emit_remainder;                  // :175
-        next_hash = hash32(uld32(sdata, next_ip), shift);
-        cand = (uint16_t)(uniform(stab[cur_hash]) + 1);                        // :190
-        if (lane == 0) stab[cur_hash] = (uint16_t)(ip - 1);                    // :191
-        if (uld32(sdata, cand) == uld32(sdata, ip)) break;                     // :193
+      // literal search, 64 probes per step (:167-194)
+      const uint32_t p0 = ip;
+      bool found = false;
+      for (uint32_t k0 = 0; k0 < kMaxProbes; k0 += kWave) {
+        const uint32_t p = p0 + sD[k0 + lane];
+        const bool valid = (int32_t)(p0 + sD[k0 + lane + 1]) <= ip_limit;     // :175
+        const uint32_t cur = valid ? lds_ld32(sdata, p) : 0u;
+        const uint32_t h = hash32(cur, shift);
+        uint32_t r = 0;
+        if (valid) r = __hip_atomic_fetch_max(&stab[h], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t c = r ? r - 1 : 0u;                                     // :190
+        const bool hit = valid && lds_ld32(sdata, c) == cur;                   // :193
+        const uint64_t hm = ballot(hit);
+        if (hm) {
+          const uint32_t j = ctz64(hm);
+          const uint32_t pj = readlane(p, j);
+          if (valid && lane > j && r <= pj + 1) stab[h] = r;                   // undo later probes
+          ip = pj;
+          cand = readlane(c, j);
+          found = true;
+          break;
+        }
+        if (ballot(valid) != ~0ull) break;                                     // :175 -> remainder
       }
+      if (!found) goto emit_remainder;
       op = emit_literal_g(dst, op, sdata, next_emit, ip - next_emit, lane, true);   // :200
       for (;;) {                                                               // :211-239
         uint32_t avail = e - (ip + 4) + 1;
@@ -139,9 +172,10 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         uint32_t prev_hash = hash32(uld32(sdata, ip - 1), shift);              // :228
         uint32_t input_bytes = uld32(sdata, ip);
         uint32_t cur_hash = hash32(input_bytes, shift);
-        if (lane == 0) stab[prev_hash] = (uint16_t)(ip - 2);                   // :233
-        cand = (uint16_t)(uniform(stab[cur_hash]) + 1);                        // :234
-        if (lane == 0) stab[cur_hash] = (uint16_t)(ip - 1);                    // :235
+        if (lane == 0) stab[prev_hash] = ip;                                   // :233 (pos ip-1)
+        const uint32_t rv = uniform(stab[cur_hash]);                           // :234
+        cand = rv ? rv - 1 : 0u;
+        if (lane == 0) stab[cur_hash] = ip + 1;                                // :235 (pos ip)
         if (input_bytes != uld32(sdata, cand)) break;                          // :238
       }
     }
