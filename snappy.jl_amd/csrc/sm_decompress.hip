@@ -35,8 +35,33 @@
 #ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only)
 #define SM_ABLATE_D 0
 #endif
+#ifndef SM_STAMP     // diagnostic builds only: per-section s_memtime stamps (tools/stamp_run.py)
+#define SM_STAMP 0
+#endif
 
 namespace sm {
+
+#if SM_STAMP
+__device__ unsigned long long g_stamp[8];
+#define STAMP_DECL                         \
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  uint64_t st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                        \
+  {                                                     \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    st_acc[i] += t_ - st_t;                             \
+    st_t = t_;                                          \
+  }
+#define STAMP_COUNT(i, v) st_acc[i] += (v);
+#define STAMP_FLUSH \
+  if (lane == 0)    \
+    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_stamp[i_], (unsigned long long)st_acc[i_]);
+#else
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_COUNT(i, v)
+#define STAMP_FLUSH
+#endif
 
 typedef uint16_t __attribute__((aligned(1))) du16u;
 typedef uint32_t __attribute__((aligned(1))) du32u;
@@ -118,25 +143,6 @@ __device__ int32_t decode_stream_global(const uint8_t* __restrict__ in, uint32_t
 // ---------------------------------------------------------------------------------------
 // batched tag engine
 
-// write the low `cnt` (0..8) bytes of v at out[o] (global)
-__device__ inline void store_partial(uint8_t* out, uint32_t o, uint64_t v, uint32_t cnt) {
-  if (cnt >= 8) {
-    *reinterpret_cast<du64u*>(out + o) = v;
-    return;
-  }
-  if (cnt & 4) {
-    *reinterpret_cast<du32u*>(out + o) = (uint32_t)v;
-    o += 4;
-    v >>= 32;
-  }
-  if (cnt & 2) {
-    *reinterpret_cast<du16u*>(out + o) = (uint16_t)v;
-    o += 2;
-    v >>= 16;
-  }
-  if (cnt & 1) out[o] = (uint8_t)v;
-}
-
 // size of a tag starting with byte c followed by `trailer` (u8; 255 = long literal)
 __device__ inline uint32_t spec_size(uint32_t c, uint32_t trailer) {
   uint32_t entry = char_entry(c);
@@ -148,7 +154,7 @@ __device__ inline uint32_t spec_size(uint32_t c, uint32_t trailer) {
   return lit > 200 ? 255u : 1 + taglen + lit;
 }
 
-__device__ inline uint32_t pack_sizes(uint32_t cur, uint32_t nxt) {
+__device__ inline uint32_t pack_sizes_slow(uint32_t cur, uint32_t nxt) {
   uint32_t s = 0;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -157,6 +163,20 @@ __device__ inline uint32_t pack_sizes(uint32_t cur, uint32_t nxt) {
     s |= spec_size(c, tr) << (8 * j);
   }
   return s;
+}
+
+// Speculative sizes of tags starting at the 4 bytes of cur (nxt = the 4 bytes after), packed
+// u8, in SWAR: copy-1/2/4 sizes by a v_perm_b32 byte lookup on the kind bits, short literals
+// (len < 61) as hi + 2 per byte.  Only a lane holding a literal tag with length bytes (hi >=
+// 60: rare in text, ~6% of lanes on random bytes) takes the per-byte path.  Equal to
+// pack_sizes_slow for every input (tools/check_tag_sizes.c, run by tests/test_host_logic.py).
+__device__ inline uint32_t pack_sizes(uint32_t cur, uint32_t nxt) {
+  const uint32_t K = cur & 0x03030303u, H = (cur >> 2) & 0x3f3f3f3fu;
+  const uint32_t csz = __builtin_amdgcn_perm(0u, 0x05030200u, K);       // kind 1/2/3 -> 2/3/5
+  const uint32_t nz = ((K + 0x7f7f7f7fu) & 0x80808080u) >> 7;          // 1 per copy byte
+  const uint32_t ml = (nz ^ 0x01010101u) * 0xffu;                       // 0xff per literal byte
+  const uint32_t sz = (csz & ~ml) | ((H + 0x02020202u) & ml);
+  return ((H + 0x44444444u) & 0x80808080u & ml) ? pack_sizes_slow(cur, nxt) : sz;
 }
 
 // ring slot write: stream bytes [base, base+256) (word per lane) at ring[(base & 1023)]
@@ -169,22 +189,99 @@ __device__ inline void ring_put(uint8_t* ring, uint32_t base, uint32_t word, uin
 // 8 stream bytes at pos (aligned dword reads: the mirror covers the 12 bytes past kRing)
 __device__ inline uint64_t ring_get8(const uint8_t* ring, uint32_t pos) { return lds_ld64(ring, pos & (kRing - 1)); }
 
+// ring refill at wb: slots [wb, wb+768) and the two prefetch words, all five loads in flight
+__device__ inline void ring_fill(const uint8_t* __restrict__ in, uint32_t N, uint32_t wb, uint8_t* ring, uint32_t& pre1,
+                                 uint32_t& pre2, uint32_t lane) {
+  uint32_t w[5];
+  if ((((uintptr_t)(in + wb)) & 3) == 0 && wb + 1280 <= N) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(in + wb) + lane;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) w[i] = s[64 * i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) w[i] = load_word(in, N, wb + 256 * i + 4 * lane);
+  }
+  ring_put(ring, wb, w[0], lane);
+  ring_put(ring, wb + 256, w[1], lane);
+  ring_put(ring, wb + 512, w[2], lane);
+  pre1 = w[3];
+  pre2 = w[4];
+}
+
+// ---- LDS output window --------------------------------------------------------------------
+// The last kWin output bytes of the stream live in a per-wave LDS ring (position x at
+// x mod kWin) besides going to HBM.  Copies whose offset is <= kLdsSrc read their source
+// there, so a batch's dependency rounds cost LDS latency, not an HBM store->load round trip;
+// HBM gets the output in 16-byte blocks when a batch ends (no partial stores).  A batch writes
+// at most kBatchOut bytes, so a source at distance <= kLdsSrc is never overwritten by the
+// batch's own output (kLdsSrc + kBatchOut + margin <= kWin).  Bytes are written with aligned
+// ds_or_b64 pairs into bytes zeroed when the batch starts (a misaligned LDS write/read costs a
+// cycle per lane, tools/lds_bench.hip).
+constexpr uint32_t kWin = 4096;
+constexpr uint32_t kBatchOut = 1024;
+constexpr uint32_t kLdsSrc = kWin - kBatchOut - 64;
+
+__device__ inline uint64_t win_get8(const uint8_t* win, uint32_t x) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(win);
+  const uint32_t sl = x & (kWin - 1), i = sl >> 3, sh = 8 * (sl & 7);
+  const uint64_t lo = w[i], hi = w[(i + 1) & (kWin / 8 - 1)];
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+
+// OR the low cnt (1..8) bytes of v into the (zeroed) window at output position x
+__device__ inline void win_put8(uint8_t* win, uint32_t x, uint64_t v, uint32_t cnt) {
+  if (cnt < 8) v &= (1ull << (8 * cnt)) - 1;
+  uint64_t* w = reinterpret_cast<uint64_t*>(win);
+  const uint32_t sl = x & (kWin - 1), i = sl >> 3, sh = 8 * (sl & 7);
+  __hip_atomic_fetch_or(&w[i], v << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (sh && sh + 8 * cnt > 64)
+    __hip_atomic_fetch_or(&w[(i + 1) & (kWin / 8 - 1)], v >> (64 - sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// zero the window bytes of positions [x, x+len) (to the end of the last 8-byte word), keeping
+// the bytes below x in its word
+__device__ inline void win_zero(uint8_t* win, uint32_t x, uint32_t len, uint32_t lane) {
+  uint64_t* w = reinterpret_cast<uint64_t*>(win);
+  const uint32_t sl = x & (kWin - 1);
+  if ((sl & 7) && lane == 0)
+    __hip_atomic_fetch_and(&w[sl >> 3], (1ull << (8 * (sl & 7))) - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const uint32_t f = (sl + 7) >> 3, e = (sl + len + 7) >> 3;
+  for (uint32_t k = f + lane; k < e; k += kWave) w[k & (kWin / 8 - 1)] = 0;
+}
+
+// HBM gets the window bytes of output positions [from, to): head bytes up to a 16-byte
+// position boundary, 16-byte blocks, tail bytes
+__device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t from, uint32_t to, uint32_t lane) {
+  if (to <= from) return;
+  const uint32_t h = min((16u - (from & 15u)) & 15u, to - from);
+  if (lane < h) out[from + lane] = win[(from + lane) & (kWin - 1)];
+  from += h;
+  const uint32_t nb = (to - from) >> 4;
+  for (uint32_t k = lane; k < nb; k += kWave) {
+    const uint32_t x = from + 16 * k;
+    const uint4 v = *reinterpret_cast<const uint4*>(win + (x & (kWin - 1)));
+    *reinterpret_cast<du64u*>(out + x) = ((uint64_t)v.y << 32) | v.x;
+    *reinterpret_cast<du64u*>(out + x + 8) = ((uint64_t)v.w << 32) | v.z;
+  }
+  from += nb << 4;
+  if (lane < to - from) out[from + lane] = win[(from + lane) & (kWin - 1)];
+}
+
 __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t size,
-                                       uint8_t* out, uint8_t* ring, uint16_t* jt, uint32_t lane) {
+                                       uint8_t* out, uint8_t* ring, uint16_t* jt, uint8_t* win, uint32_t lane) {
   // ring holds stream bytes [wb, wb+768); pre1 = [wb+768, wb+1024) (loaded a batch ago),
   // pre2 = [wb+1024, wb+1280) issued at the end of the previous batch -- so a round's fence
   // (s_waitcnt vmcnt(0)) never waits for a freshly issued prefetch.
   uint32_t wb = ip & ~255u;
-  ring_put(ring, wb, load_word(in, N, wb + 4 * lane), lane);
-  ring_put(ring, wb + 256, load_word(in, N, wb + 256 + 4 * lane), lane);
-  ring_put(ring, wb + 512, load_word(in, N, wb + 512 + 4 * lane), lane);
-  uint32_t pre1 = load_word(in, N, wb + 768 + 4 * lane);
-  uint32_t pre2 = load_word(in, N, wb + 1024 + 4 * lane);
+  uint32_t pre1, pre2;
+  ring_fill(in, N, wb, ring, pre1, pre2, lane);
   bool issue_pre2 = false;
-  uint32_t op = 0;
+  uint32_t op = 0, flushed = 0;  // output produced / already in HBM
   const int64_t Nm1 = (int64_t)N - 1;
 
+  STAMP_DECL
   while ((int64_t)ip < Nm1) {
+    STAMP_COUNT(6, 1)
     if (ip >= wb + 256) {
       if (ip < wb + 512) {
         ring_put(ring, wb + 768, pre1, lane);
@@ -193,14 +290,11 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         issue_pre2 = true;  // [wb+1024, wb+1280) loads after this batch
       } else {  // jumped (long literal): refill
         wb = ip & ~255u;
-        ring_put(ring, wb, load_word(in, N, wb + 4 * lane), lane);
-        ring_put(ring, wb + 256, load_word(in, N, wb + 256 + 4 * lane), lane);
-        ring_put(ring, wb + 512, load_word(in, N, wb + 512 + 4 * lane), lane);
-        pre1 = load_word(in, N, wb + 768 + 4 * lane);
-        pre2 = load_word(in, N, wb + 1024 + 4 * lane);
+        ring_fill(in, N, wb, ring, pre1, pre2, lane);
         issue_pre2 = false;
       }
     }
+    STAMP(0)
     // speculative tag sizes for the window [ip, ip+256) (inside the ring: ip < wb+256; a
     // batch's literals end before ip+256+200 < wb+768)
     const uint64_t cw = ring_get8(ring, ip + 4 * lane);
@@ -263,18 +357,20 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
     }
     const uint32_t ntok = nvalid < 64 ? nvalid : 64;
-    uint32_t tpos = 0, ipw = ip;
+    uint32_t tpos = 0, ipw = ip, tnext = 0;
     bool big = false;
     if (ntok) {
       const uint32_t sv = reinterpret_cast<const uint32_t*>(jt)[lane < ntok ? lane : 0];
       tpos = ip + (sv & 0xffff);
-      ipw = ip + readlane(sv >> 16, ntok - 1);
+      tnext = sv >> 16;
+      ipw = ip + readlane(tnext, ntok - 1);
     }
     if (ipw < wlim) {
       const uint32_t rel = ipw - ip;
       big = ((readlane(sizes, rel >> 2) >> ((rel & 3) * 8)) & 0xff) == 255;
     }
 
+    STAMP(1)
     if (ntok) {
       const bool mine = lane < ntok;
       const uint64_t hv = ring_get8(ring, mine ? tpos : wb);
@@ -305,11 +401,23 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
       const uint64_t em = ballot(err != kOk);
       if (em) return (int32_t)readlane((uint32_t)err, ctz64(em));
+      // cap the batch output at kBatchOut bytes (the window bound); one tag is <= 200 B
+      uint32_t nt = ntok;
+      if (readlane(incl, ntok - 1) > kBatchOut) {
+        nt = (uint32_t)__builtin_popcountll(ballot(mine && incl <= kBatchOut));
+        ipw = ip + readlane(tnext, nt - 1);
+        big = false;  // the next tag is a batch tag inside the window
+      }
+      const bool act_t = lane < nt;
+      const uint32_t X = readlane(incl, nt - 1);
+      STAMP(2)
 
+      win_zero(win, op, X, lane);
       // dependencies: tfirst = last tag u < t whose output starts at or before the source start
       const uint32_t O0 = op;
       const uint32_t slo = opt - offset;
       const uint32_t shi = slo + min(len, offset);
+      const bool gsrc = iscopy && offset > kLdsSrc;  // source older than the window: from HBM
       uint32_t lo = 0, hi = lane ? lane - 1 : 0;
 #pragma unroll
       for (int it = 0; it < 6; ++it) {
@@ -321,33 +429,34 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         }
       }
       const uint32_t tfirst = lo;
-      const uint64_t all = ntok == 64 ? ~0ull : ((1ull << ntok) - 1);
+      const uint64_t all = nt == 64 ? ~0ull : ((1ull << nt) - 1);
       const bool longlit = !iscopy && litlen > 64;
       uint64_t done = (ballot(longlit) & all) | ~all;
+      // HBM sources: this wave's earlier flushes (and big literals) must have landed
+      if (ballot(act_t && gsrc)) __threadfence_block();
 
-      // long literals (65..200 B, no dependencies, still inside the ring window): one whole-wave
-      // pass each, 8 bytes per lane
-      uint64_t lm = ballot(mine && longlit);
+      // long literals (65..200 B, no dependencies, inside the input ring): whole-wave passes
+      uint64_t lm = ballot(act_t && longlit);
       while (lm) {
         const uint32_t t = ctz64(lm);
         lm &= lm - 1;
-        const uint32_t o = readlane(opt, t), s = readlane(lsrc, t), L = readlane(litlen, t);
+        const uint32_t o = readlane(opt, t), sr = readlane(lsrc, t), L = readlane(litlen, t);
         const uint32_t k = 8 * lane;
-        if (k < L) store_partial(out, o + k, ring_get8(ring, s + k), L - k);
+        if (k < L) win_put8(win, o + k, ring_get8(ring, sr + k), min(8u, L - k));
       }
 
-      // Dependency rounds.  A round's stores never touch bytes another ready tag of the round
-      // reads (a source overlapping this round's output makes its tag wait), so each pass of
-      // kPass chunks issues its loads, then its stores:
-      //  * literal (<= 64 B): 8-byte pieces of the LDS ring;
+      STAMP(3)
+      // One round (all in LDS) runs every tag whose source is final before the batch (or only
+      // needs the long literals above); its writes never touch bytes another ready tag reads:
+      //  * literal (<= 64 B): 8-byte pieces of the input ring;
       //  * copy: its source window S = out[slo, slo+offset) is final when the round starts, and
       //    output byte j is S[j mod offset] (incremental_copy_slow!, internal.jl:477-481), so
       //    chunk i = S from phase m = 8i mod offset, wrapping once to S's start (offset >= 8);
       //    for offset < 8 the period is unrolled to 16 bytes in registers.
       const uint64_t range = lane > tfirst ? (((1ull << lane) - 1) & ~((1ull << tfirst) - 1)) : 0ull;
       if (SM_ABLATE_D & 1) done = ~0ull;
-      while (done != ~0ull) {
-        __threadfence_block();  // this wave's earlier stores land before the loads below
+      if (done != ~0ull) {
+        STAMP_COUNT(7, 1)
         const bool ready = !((done >> lane) & 1) &&
                            ((SM_ABLATE_D & 2) || !iscopy || shi <= O0 || ((~done) & range) == 0);
         const uint64_t rm = ballot(ready);
@@ -362,13 +471,14 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
               for (int i = 0; i < kPass; ++i)
                 v[i] = base + 8 * i < L ? ring_get8(ring, lsrc + base + 8 * i) : 0ull;
             } else if (offset >= 8) {
-              const uint64_t B = *reinterpret_cast<const du64u*>(out + slo);
+              const uint64_t B = gsrc ? *reinterpret_cast<const du64u*>(out + slo) : win_get8(win, slo);
               uint32_t m0 = base;
               while (m0 >= offset) m0 -= offset;
               uint32_t m = m0;
 #pragma unroll
               for (int i = 0; i < kPass; ++i) {
-                v[i] = base + 8 * i < L ? *reinterpret_cast<const du64u*>(out + slo + m) : 0ull;
+                v[i] = base + 8 * i < L ? (gsrc ? *reinterpret_cast<const du64u*>(out + slo + m) : win_get8(win, slo + m))
+                                        : 0ull;
                 m += 8;
                 if (m >= offset) m -= offset;
               }
@@ -381,7 +491,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
                 if (m >= offset) m -= offset;
               }
             } else {
-              const uint64_t x = *reinterpret_cast<const du64u*>(out + slo);
+              const uint64_t x = win_get8(win, slo);
               uint64_t p0 = x & ((1ull << (8 * offset)) - 1);
               for (uint32_t have = offset; have < 8; have *= 2) p0 |= p0 << (8 * have);
               // p0 = S repeated over 8 bytes; p1 = the next 8 bytes of the period
@@ -401,12 +511,35 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
             }
 #pragma unroll
             for (int i = 0; i < kPass; ++i)
-              if (base + 8 * i < L) store_partial(out, opt + base + 8 * i, v[i], L - base - 8 * i);
+              if (base + 8 * i < L) win_put8(win, opt + base + 8 * i, v[i], min(8u, L - base - 8 * i));
           }
         }
         done |= rm;
       }
-      op += readlane(incl, ntok - 1);
+      // The copies left (a few per batch: their source overlaps earlier tags of this batch) run
+      // in stream order, one tag at a time, a byte per lane: byte k = S[k mod offset] with S
+      // final by then (LDS accesses of a wave are serviced in order).
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      uint64_t rest = ~done;
+      while (rest) {
+        const uint32_t t = ctz64(rest);
+        rest &= rest - 1;
+        STAMP_COUNT(7, 1)
+        const uint32_t o = readlane(opt, t), sl = readlane(slo, t), L = readlane(len, t), off = readlane(offset, t);
+        if (lane < L) {
+          uint32_t k = lane;
+          if (k >= off) {  // k mod off for k, off <= 64: exact through the f32 reciprocal
+            const uint32_t q = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)off));
+            k -= q * off;
+          }
+          win[(o + lane) & (kWin - 1)] = win[(sl + k) & (kWin - 1)];
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      }
+      STAMP(4)
+      op += X;
+      win_flush(out, win, flushed, op & ~15u, lane);  // whole 16-byte blocks to HBM
+      flushed = max(flushed, op & ~15u);
       ip = ipw;
     }
     if (issue_pre2) {
@@ -415,7 +548,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     }
 
     if (big) {
-      // one literal too long for the batch path (or a wrapped length): scalar decode
+      // one literal too long for the batch path (or a wrapped length): straight to HBM
       const uint64_t hv = ring_get8(ring, ip);
       const uint32_t c = uniform((uint32_t)hv & 0xff);
       const uint32_t entry = char_entry(c);
@@ -427,6 +560,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const int64_t avail_out = (int64_t)size - (int64_t)op;
       const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
       if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) return kErrLiteral;  // :518
+      win_flush(out, win, flushed, op, lane);  // HBM holds everything before the literal
       // bulk copy: head bytes to 16-B source alignment, then 16 B per lane, 4 in flight
       const uint8_t* s = in + lsrc;
       uint32_t head = (uint32_t)((16 - ((uintptr_t)s & 15)) & 15);
@@ -454,10 +588,29 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
       const uint32_t done16 = head + (n16 << 4);
       if (lane < litlen - done16) out[op + done16 + lane] = s[done16 + lane];
+      // the window keeps the literal's tail, which later copies may read
+      const uint32_t keep = min(litlen, kLdsSrc + 64);
+      const uint32_t t0 = op + litlen - keep;
+      win_zero(win, t0, keep, lane);
+      for (uint32_t x = 8 * lane; x < keep; x += 8 * kWave) {
+        const uint8_t* q = s + (t0 - op) + x;
+        const uint32_t cnt = min(8u, keep - x);
+        uint64_t v = 0;
+        if (cnt == 8) {
+          v = *reinterpret_cast<const du64u*>(q);
+        } else {  // the literal's last bytes: never read past the stream
+          for (uint32_t i = 0; i < cnt; ++i) v |= (uint64_t)q[i] << (8 * i);
+        }
+        win_put8(win, t0 + x, v, cnt);
+      }
       op += litlen;
+      flushed = op;
       ip = lsrc + litlen;
     }
   }
+  win_flush(out, win, flushed, op, lane);
+  STAMP(5)
+  STAMP_FLUSH
   if (op != size) return kErrInvalid;                                    // Snappy.jl:50
   return kOk;
 }
@@ -465,6 +618,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
 __global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
   __shared__ __attribute__((aligned(16))) uint16_t sjt[kWalkLevels * 256];  // tag-walk jump tables
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];                // output window
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
   const uint8_t* in = a.in + a.in_off[b];
@@ -497,7 +651,7 @@ __global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
   if (st == kOk && size > cap) st = kBufferTooSmall;
   if (st == kOk) {
     if (size <= kBlockSize) {
-      st = decode_stream_batch(in, N, ip, size, dst, sring, sjt, lane);
+      st = decode_stream_batch(in, N, ip, size, dst, sring, sjt, swin, lane);
     } else {
       st = decode_stream_global(in, N, ip, size, dst, lane);
     }
@@ -513,5 +667,16 @@ hipError_t launch_decompress(const DecompressArgs& a, int /*large*/, hipStream_t
   hipLaunchKernelGGL(k_decompress, dim3(a.nblk), dim3(64), 0, s, a);
   return hipGetLastError();
 }
+
+#if SM_STAMP
+extern "C" int sm_debug_stamps(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(g_stamp)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 }  // namespace sm

@@ -1,0 +1,59 @@
+"""Decoder section timing from in-kernel s_memtime stamps (design tool, GPU box).
+
+Build the diagnostic library, then run:
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DSM_STAMP=1 -o tools/abl/lib_stamp.so \
+      snappy.jl_amd/csrc/sm_*.hip
+  SNAPPY_MI355X_LIB=tools/abl/lib_stamp.so python3 tools/stamp_run.py [--data text|random]
+Sections (per wave, summed over all streams): 0 ring management, 1 tag walk (sizes, doubling,
+descent, compaction), 2 per-tag decode + error checks, 3 dependency search + long literals,
+4 execution rounds, 5 prefetch issue + big literals + tail; 6 = batches, 7 = rounds.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+NAMES = ["ring", "walk", "decode", "deps+longlit", "rounds", "prefetch+big+tail"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=4000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--data", default="text")
+    args = ap.parse_args()
+    sm = bench.load_package()
+    lib = sm.lib()
+    fn = lib.sm_debug_stamps
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    dev = torch.device("cuda", 0)
+    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 7)
+    b = bench.Batch(blocks, dev)
+    b.compress(sm, "fast")
+    b.uncompress(sm)
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 8)()
+    fn(buf, 1)
+    for _ in range(args.reps):
+        b.uncompress(sm)
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    v = list(buf)
+    tot = sum(v[:6])
+    batches, rounds = v[6], v[7]
+    print("data %s: %d batches (%.1f per block), %d rounds (%.2f per batch)" % (
+        args.data, batches, batches / args.blocks / args.reps, rounds, rounds / max(batches, 1)))
+    for i, nme in enumerate(NAMES):
+        print("  %-18s %5.1f%%  %8.0f cycles/batch" % (nme, 100.0 * v[i] / tot, v[i] / max(batches, 1)))
+    print("  total              %8.0f cycles/batch" % (tot / max(batches, 1)))
+    print("roundtrip ok:", b.verify())
+
+
+if __name__ == "__main__":
+    main()
