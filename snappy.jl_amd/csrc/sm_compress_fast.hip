@@ -33,6 +33,11 @@
 
 namespace sm {
 
+#if SM_STAMP
+__device__ unsigned long long g_stamp_c[12];
+#endif
+STAMP_MACROS(12)
+
 constexpr uint32_t kFTabBits = 14;
 constexpr uint32_t kFTab = 1u << kFTabBits;   // shared table entries
 constexpr uint32_t kPrivBits = 8;
@@ -126,12 +131,12 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     uint4* d16 = reinterpret_cast<uint4*>(data);
     const uint32_t n16 = n >> 4;
     if (n16 == kBlockSize / 16) {
-      constexpr int kStage = kBlockSize / 16 / kThreads;
-      uint4 v[kStage];
+      constexpr int kLoads = kBlockSize / 16 / kThreads;
+      uint4 v[kLoads];
 #pragma unroll
-      for (int i = 0; i < kStage; ++i) v[i] = s16[tid + i * kThreads];
+      for (int i = 0; i < kLoads; ++i) v[i] = s16[tid + i * kThreads];
 #pragma unroll
-      for (int i = 0; i < kStage; ++i) d16[tid + i * kThreads] = v[i];
+      for (int i = 0; i < kLoads; ++i) d16[tid + i * kThreads] = v[i];
     } else {
       for (uint32_t k = tid; k < n16; k += kThreads) d16[k] = s16[k];
       for (uint32_t k = (n & ~15u) + tid; k < n; k += kThreads) data[k] = src[k];
@@ -167,7 +172,9 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     }
   }
 
+  STAMP_DECL
   for (uint32_t r = 0; r < rounds; ++r) {
+    STAMP_COUNT(11, 1)
     const uint32_t k = r * kWavesPerBlock + wave;
     const bool active = k < nchunks;
     const uint32_t c0 = k * kChunk;
@@ -187,7 +194,9 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         }
       }
     }
+    STAMP(0)
     __syncthreads();  // B1
+    STAMP(1)
 
     // (b) candidates, verify, extend, walk, sizes
     uint32_t ta = 0, tb = 0, ntok = 0, incl = 0, sz = 0, litlen = 0, littag = 0, ls = 0;
@@ -250,6 +259,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         Ls[j] = (SM_ABLATE & 2) ? 0u : L;
         offs[j] = q - c;
       }
+      STAMP(2)
       // finish matches that filled the eager window: 8 bytes per lane per step
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -267,6 +277,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         }
         Ls[j] = L;
       }
+      STAMP(3)
       // Greedy parse by pointer doubling (no serial loop) over the chunk's 128 positions.
       // J0 skips literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a
       // non-match), else the chunk end, so the greedy walk from 0 steps only between copies
@@ -305,6 +316,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
           }
         }
       }
+      STAMP(4)
       const bool tok0 = cur[0] == lane && Ls[0] != 0;
       const bool tok1 = cur[1] == 64 + lane && Ls[1] != 0;
       ts0 = ballot(tok0);
@@ -355,6 +367,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       if (lane == 0) csize[wave] = 0;
     }
 
+    STAMP(5)
     // next round: words and first-chance candidates (table as of this round)
     uint64_t wn[2];
     uint32_t t1n[2];
@@ -368,7 +381,9 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         t1n[j] = k2 < nchunks ? T[((uint32_t)wn[j] * kHashMul) >> (32 - kFTabBits)] : 0;
       }
     }
+    STAMP(6)
     __syncthreads();  // B2
+    STAMP(7)
 
     // (c) round layout, lane-parallel over the round's chunks (lane u = chunk u): a literal
     // run that crosses chunk boundaries inside the round is emitted once, with one tag for
@@ -409,6 +424,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       mycont = readlane((uint32_t)cont_in, wave);
       myrun = readlane(runlen, wave);
     }
+    STAMP(8)
     if (active && !(SM_ABLATE & 1)) {
       const uint32_t rm = mycont ? readlane(littag, 0) : 0u;                 // leading tag removed
       const uint32_t tq = c0 + (ta & 0xffff), tL = ta >> 16;
@@ -437,6 +453,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         below += __builtin_popcountll(ts);
       }
     }
+    STAMP(9)
     op += total;
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -444,8 +461,21 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       t1[j] = t1n[j];
     }
   }
+  STAMP(10)
+  STAMP_FLUSH(g_stamp_c)
   if (tid == 0) a.out_len[b] = op;
 }
+
+#if SM_STAMP
+extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_c), sizeof(g_stamp_c)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[12] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_c), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 constexpr size_t kFastLds =
     kBlockSize + 4 * (kFTab + kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * kLevels * kChunk;

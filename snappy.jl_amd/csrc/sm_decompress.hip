@@ -35,33 +35,13 @@
 #ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only)
 #define SM_ABLATE_D 0
 #endif
-#ifndef SM_STAMP     // diagnostic builds only: per-section s_memtime stamps (tools/stamp_run.py)
-#define SM_STAMP 0
-#endif
 
 namespace sm {
 
 #if SM_STAMP
 __device__ unsigned long long g_stamp[8];
-#define STAMP_DECL                         \
-  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
-  uint64_t st_t = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                        \
-  {                                                     \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
-    st_acc[i] += t_ - st_t;                             \
-    st_t = t_;                                          \
-  }
-#define STAMP_COUNT(i, v) st_acc[i] += (v);
-#define STAMP_FLUSH \
-  if (lane == 0)    \
-    for (int i_ = 0; i_ < 8; ++i_) atomicAdd(&g_stamp[i_], (unsigned long long)st_acc[i_]);
-#else
-#define STAMP_DECL
-#define STAMP(i)
-#define STAMP_COUNT(i, v)
-#define STAMP_FLUSH
 #endif
+STAMP_MACROS(8)
 
 typedef uint16_t __attribute__((aligned(1))) du16u;
 typedef uint32_t __attribute__((aligned(1))) du32u;
@@ -610,7 +590,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   }
   win_flush(out, win, flushed, op, lane);
   STAMP(5)
-  STAMP_FLUSH
+  STAMP_FLUSH(g_stamp)
   if (op != size) return kErrInvalid;                                    // Snappy.jl:50
   return kOk;
 }

@@ -8,6 +8,34 @@
 
 namespace sm {
 
+// Diagnostic builds only (-DSM_STAMP=1, tools/stamp_run.py): per-wave s_memtime section
+// stamps, summed into a device array by lane 0 when a wave finishes.
+#ifndef SM_STAMP
+#define SM_STAMP 0
+#endif
+#if SM_STAMP
+#define STAMP_MACROS(NS) constexpr int kStampSlots = NS;
+#define STAMP_DECL                                \
+  uint64_t st_acc[kStampSlots] = {};              \
+  uint64_t st_t = __builtin_amdgcn_s_memtime();
+#define STAMP(i)                                      \
+  {                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[i] += t_ - st_t;                           \
+    st_t = t_;                                        \
+  }
+#define STAMP_COUNT(i, v) st_acc[i] += (v);
+#define STAMP_FLUSH(arr) \
+  if (lane == 0)         \
+    for (int i_ = 0; i_ < kStampSlots; ++i_) atomicAdd(&arr[i_], (unsigned long long)st_acc[i_]);
+#else
+#define STAMP_MACROS(NS)
+#define STAMP_DECL
+#define STAMP(i)
+#define STAMP_COUNT(i, v)
+#define STAMP_FLUSH(arr)
+#endif
+
 constexpr uint32_t kBlockSize = 65536;        // internal.jl:31
 constexpr uint32_t kInputMarginBytes = 15;    // internal.jl:32
 constexpr uint32_t kMaxHashTableSize = 16384; // internal.jl:33

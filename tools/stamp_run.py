@@ -4,7 +4,8 @@ Build the diagnostic library, then run:
   hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -DSM_STAMP=1 -o tools/abl/lib_stamp.so \
       snappy.jl_amd/csrc/sm_*.hip
   SNAPPY_MI355X_LIB=tools/abl/lib_stamp.so python3 tools/stamp_run.py [--data text|random]
-Sections (per wave, summed over all streams): 0 ring management, 1 tag walk (sizes, doubling,
+  ... --op compress_fast: the fast compressor's per-round sections instead.
+Decoder sections (per wave, summed over all streams): 0 ring management, 1 tag walk (sizes, doubling,
 descent, compaction), 2 per-tag decode + error checks, 3 dependency search + long literals,
 4 execution rounds, 5 prefetch issue + big literals + tail; 6 = batches, 7 = rounds.
 """
@@ -20,6 +21,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 NAMES = ["ring", "walk", "decode", "deps+longlit", "rounds", "prefetch+big+tail"]
+CNAMES = ["inserts", "B1 wait", "candidates", "long matches", "parse", "tokens+sizes", "prefetch",
+          "B2 wait", "layout", "emission", "tail"]
 
 
 def main():
@@ -27,7 +30,10 @@ def main():
     ap.add_argument("--blocks", type=int, default=4000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--data", default="text")
+    ap.add_argument("--op", default="uncompress", choices=["uncompress", "compress_fast"])
     args = ap.parse_args()
+    if args.op == "compress_fast":
+        return compress_stamps(args)
     sm = bench.load_package()
     lib = sm.lib()
     fn = lib.sm_debug_stamps
@@ -53,6 +59,30 @@ def main():
         print("  %-18s %5.1f%%  %8.0f cycles/batch" % (nme, 100.0 * v[i] / tot, v[i] / max(batches, 1)))
     print("  total              %8.0f cycles/batch" % (tot / max(batches, 1)))
     print("roundtrip ok:", b.verify())
+
+
+def compress_stamps(args):
+    sm = bench.load_package()
+    fn = sm.lib().sm_debug_stamps_c
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    dev = torch.device("cuda", 0)
+    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 7)
+    b = bench.Batch(blocks, dev)
+    b.compress(sm, "fast")
+    torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 12)()
+    fn(buf, 1)
+    for _ in range(args.reps):
+        b.compress(sm, "fast")
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    v = list(buf)
+    rounds = v[11]
+    tot = sum(v[:11])
+    print("compress_fast %s: %d wave-rounds" % (args.data, rounds))
+    for i, nme in enumerate(CNAMES):
+        print("  %-14s %5.1f%%  %7.0f cycles/wave-round" % (nme, 100.0 * v[i] / tot, v[i] / max(rounds, 1)))
+    print("  total          %7.0f cycles/wave-round" % (tot / max(rounds, 1)))
 
 
 if __name__ == "__main__":
