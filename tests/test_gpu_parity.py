@@ -230,3 +230,47 @@ def test_decompress_large_stream_global_path(sm, oracle, gpu_available):
     raw = read_testfile("html_x_4") + read_testfile("urls.10K")[:100000]
     comp = oracle.compress(raw)
     assert sm.uncompress(comp) == raw
+
+
+# ---- decoder edge cases on hand-built streams (tests/streams.py) -------------------------
+
+def _decode_all(sm, streams):
+    outs, status = sm.uncompress_batch(streams)
+    assert not np.asarray(status).any()
+    return outs
+
+
+def test_decompress_window_boundaries(sm, oracle, gpu_available):
+    """Copies into long literals and across the LDS output window's reach (kLdsSrc = 3008:
+    nearer sources are read from LDS, farther ones from HBM), overlapping copies after a
+    long literal, and a batch whose output exceeds the 1 KiB batch cap."""
+    from streams import build
+    rng = np.random.default_rng(3)
+    big = rng.integers(0, 256, 5000, dtype=np.uint8).tobytes()
+    cases = []
+    for off in (1, 2, 7, 8, 15, 16, 17, 64, 100, 999, 2047, 2048, 3006, 3007, 3008, 3009, 3010, 4000, 4095,
+                4096, 4097, 4999, 5000):
+        for ln in (1, 4, 11, 12, 16, 33, 64):
+            cases.append([("lit", big), ("copy", off, ln), ("copy", 3, 20), ("lit", b"xyz"), ("copy", off, ln)])
+    mid = rng.integers(0, 256, 150, dtype=np.uint8).tobytes()  # a 65..200-byte literal
+    for off in (1, 5, 8, 64, 149, 150):
+        cases.append([("lit", mid), ("copy", off, 64), ("copy", off, 64)])
+    cases.append([("lit", b"ab")] + [("copy", 2, 64)] * 100)            # > 1 KiB in one batch
+    cases.append([("lit", b"a")] + [("copy", 1, 64)] * 1000)            # RLE, 64 KB
+    cases.append([("lit", big), ("lit", big[:300])] + [("copy", 4500, 64)] * 50)
+    built = [build(c) for c in cases]
+    outs = _decode_all(sm, [s for s, _ in built])
+    for (s, expect), o in zip(built, outs):
+        assert o == expect
+        assert oracle.uncompress(s) == expect
+
+
+def test_decompress_random_op_streams(sm, gpu_available):
+    """Seeded random literal/copy streams (any legal offset and length, some long
+    literals), decoded as one GPU batch against the plain LZ77 meaning of the ops."""
+    from streams import build, random_ops
+    rng = np.random.default_rng(2024)
+    built = [build(random_ops(rng, int(rng.integers(1, 65536)))) for _ in range(400)]
+    outs = _decode_all(sm, [s for s, _ in built])
+    for (s, expect), o in zip(built, outs):
+        assert o == expect

@@ -239,3 +239,13 @@ def test_hashtable_size(oracle):
     assert oracle.hashtable_size(257) == 512
     assert oracle.hashtable_size(16384) == 16384
     assert oracle.hashtable_size(10 ** 9) == 16384
+
+
+def test_stream_builder_matches_oracle_decoder(oracle):
+    """tests/streams.py (hand-built streams for the GPU decoder edge cases) agrees with the
+    oracle decoder, so its expected outputs can be trusted."""
+    from streams import build, random_ops
+    rng = np.random.default_rng(77)
+    for _ in range(20):
+        stream, expect = build(random_ops(rng, int(rng.integers(1, 40000))))
+        assert oracle.uncompress(stream) == expect
