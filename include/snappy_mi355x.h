@@ -70,6 +70,9 @@ sm_ctx* sm_ctx_create(int device);
 void sm_ctx_destroy(sm_ctx* ctx);
 /* the HIP stream the ctx launches on (hipStream_t) */
 void* sm_ctx_stream(sm_ctx* ctx);
+/* diagnostic: how the ctx's last sm_uncompress decoded -- 0 in stream order (one wave),
+ * 1 as parallel 64 KiB fragments (a large block-structured stream), -1 none yet */
+int sm_ctx_last_path(sm_ctx* ctx);
 
 /* ---- single buffer, host memory (the reference's exported API) -------------------- */
 /* replaces compress(::Vector{UInt8}), src/Snappy.jl:20-36 (and compress(::String), :38).

@@ -39,7 +39,7 @@ ABI_SYMBOLS = (
     "sm_status_message", "sm_max_compressed_length", "sm_uncompressed_length", "sm_parse32",
     "sm_encode32", "sm_ctx_create", "sm_ctx_destroy", "sm_ctx_stream", "sm_compress", "sm_uncompress",
     "sm_compress_batch_device", "sm_uncompress_batch_device", "sm_compress_batch",
-    "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device",
+    "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device", "sm_ctx_last_path",
 )
 
 
@@ -95,6 +95,8 @@ def lib():
         L.sm_compress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
         L.sm_uncompress_batch.restype = i32
         L.sm_uncompress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+        L.sm_ctx_last_path.restype = ctypes.c_int
+        L.sm_ctx_last_path.argtypes = [vp]
         L.sm_version.restype = ctypes.c_char_p
         L.sm_version.argtypes = []
         L.sm_compress_fragments_device.restype = i32
@@ -174,6 +176,11 @@ def compress(data, mode="reference", device=0):
     if st:
         raise SnappyError(st)
     return out[: ol.value].tobytes()
+
+
+def last_uncompress_path(device=0):
+    """How the last uncompress() on this device decoded: 0 in order, 1 parallel fragments."""
+    return int(lib().sm_ctx_last_path(context(device)))
 
 
 def uncompress(data, device=0):

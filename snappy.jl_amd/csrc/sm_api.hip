@@ -6,6 +6,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <vector>
 
@@ -40,7 +41,8 @@ struct DevBuf {
 struct sm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf in, out, out2, meta;
+  DevBuf in, out, out2, meta, idx;
+  int last_path = -1;  // sm_ctx_last_path
 };
 
 namespace {
@@ -59,6 +61,97 @@ struct DeviceGuard {
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+constexpr uint32_t kParallelMinOutput = 4 * 65536;  // smaller streams: one wave is as fast
+
+// Host tag walk over [p, lim) of a stream (zero-padded lookahead, internal.jl:426-462): where it
+// leaves the range and how much output the tags make.  Used when a chunk is entered deeper than
+// the entry offsets the index kernel covers.
+void host_walk(const uint8_t* comp, uint32_t n, uint64_t p, uint64_t lim, uint64_t* exit_pos, uint64_t* produced) {
+  uint64_t o = 0;
+  while (p < lim) {
+    const uint32_t c = comp[p];
+    const uint32_t entry = sm::char_entry(c);
+    const uint32_t taglen = entry >> 11;
+    uint32_t tr = 0;
+    for (uint32_t k = 0; k < 4; ++k) tr |= (p + 1 + k < n ? (uint32_t)comp[p + 1 + k] : 0u) << (8 * k);
+    const uint32_t trailer = taglen >= 4 ? tr : (tr & ((1u << (8 * taglen)) - 1u));
+    if (c & 3) {
+      p += 1 + taglen;
+      o += entry & 0xff;
+    } else {
+      const uint32_t lit = (entry & 0xff) + trailer;
+      p += 1ull + taglen + lit;
+      o += lit;
+    }
+  }
+  *exit_pos = p;
+  *produced = o;
+}
+
+// One large stream in parallel (sm_decompress.hip, "one large stream"): index pass, true path
+// on the host, one wave per 64 KiB fragment.  The compressed bytes are in ctx->in.  Returns
+// 1 with the output in ctx->out, 0 to fall back to the in-order decode, -1 on a device error.
+int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t ip0, uint32_t size) {
+  using sm::kIdxChunk;
+  using sm::kIdxEntries;
+  const uint32_t nchunks = (n - ip0 + kIdxChunk - 1) / kIdxChunk;
+  const uint32_t nfrag = (uint32_t)(((uint64_t)size + 65535) / 65536);
+  const size_t rec_n = (size_t)nchunks * kIdxEntries;
+  const size_t frag_off = align_up(2 * rec_n * 4, 16);
+  const size_t st_off = frag_off + (size_t)nfrag * sizeof(sm::StreamFrag);
+  if (ctx->idx.ensure(st_off + (size_t)nfrag * 4) != hipSuccess) return -1;
+  hipStream_t s = ctx->stream;
+  uint32_t* d_exit = (uint32_t*)ctx->idx.p;
+  uint32_t* d_out = d_exit + rec_n;
+  const uint8_t* d_in = (const uint8_t*)ctx->in.p;
+  if (sm::launch_stream_index(d_in, n, ip0, nchunks, d_exit, d_out, s) != hipSuccess) return -1;
+  std::vector<uint32_t> rec(2 * rec_n);
+  if (hipMemcpyAsync(rec.data(), d_exit, 2 * rec_n * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  // true path: chunk entries y, output before them O, output of their tags
+  struct PathChunk {
+    uint64_t y, O, out;
+  };
+  std::vector<PathChunk> path;
+  uint64_t y = ip0, O = 0;
+  while (y < (uint64_t)n - 1) {  // internal.jl:416
+    const uint64_t c = (y - ip0) / kIdxChunk, base = ip0 + c * kIdxChunk, l = y - base;
+    uint64_t ex, ot;
+    if (l < kIdxEntries) {
+      ex = rec[c * kIdxEntries + l];
+      ot = rec[rec_n + c * kIdxEntries + l];
+    } else {
+      host_walk(comp, n, y, std::min<uint64_t>(base + kIdxChunk, (uint64_t)n - 1), &ex, &ot);
+    }
+    path.push_back({y, O, ot});
+    O += ot;
+    if (O > size || ex <= y) return 0;
+    y = ex;
+  }
+  if (O != size) return 0;
+  std::vector<sm::StreamFrag> frags(nfrag);
+  size_t k = 0;
+  for (uint32_t f = 0; f < nfrag; ++f) {
+    const uint64_t F = (uint64_t)f * 65536;
+    while (k + 1 < path.size() && path[k].O + path[k].out <= F) ++k;
+    frags[f] = {(uint32_t)path[k].y, (uint32_t)path[k].O, (uint32_t)F,
+                f + 1 == nfrag ? 0xffffffffu : (uint32_t)(F + 65536)};
+  }
+  sm::StreamFrag* d_frags = (sm::StreamFrag*)((uint8_t*)ctx->idx.p + frag_off);
+  int32_t* d_st = (int32_t*)((uint8_t*)ctx->idx.p + st_off);
+  if (hipMemcpyAsync(d_frags, frags.data(), frags.size() * sizeof(sm::StreamFrag), hipMemcpyHostToDevice, s) !=
+      hipSuccess)
+    return -1;
+  if (sm::launch_decompress_frags(d_in, n, size, (uint8_t*)ctx->out.p, d_frags, nfrag, d_st, s) != hipSuccess)
+    return -1;
+  std::vector<int32_t> st(nfrag);
+  if (hipMemcpyAsync(st.data(), d_st, nfrag * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  for (int32_t v : st)
+    if (v != sm::kOk) return 0;
+  return 1;
+}
+
 }  // namespace
 
 #define SM_CHECK(x)                 \
@@ -67,6 +160,8 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
   } while (0)
 
 extern "C" {
+
+int sm_ctx_last_path(sm_ctx* ctx) { return ctx ? ctx->last_path : -1; }
 
 const char* sm_status_message(sm_status st) {
   switch (st) {
@@ -153,6 +248,7 @@ void sm_ctx_destroy(sm_ctx* ctx) {
     ctx->out.release();
     ctx->out2.release();
     ctx->meta.release();
+    ctx->idx.release();
     (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -373,6 +469,22 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   uint32_t hv[2] = {(uint32_t)n, size};
   uint64_t zero = 0;
   SM_CHECK(hipMemcpyAsync(ctx->in.p, compressed, n, hipMemcpyHostToDevice, s));
+  // a large stream: fragments in parallel when it is block-structured (Snappy.jl, libsnappy
+  // and this library all write such streams); otherwise, or on any error, the in-order decode
+  size_t hdr = 0;
+  (void)sm_parse32((const uint8_t*)compressed, n, 0, &size, &hdr);
+  if (size >= kParallelMinOutput && n - hdr >= 2 * sm::kIdxChunk) {
+    const int r = parallel_uncompress(ctx, (const uint8_t*)compressed, (uint32_t)n, (uint32_t)hdr, size);
+    if (r < 0) return SM_ERR_DEVICE;
+    if (r == 1) {
+      ctx->last_path = 1;
+      SM_CHECK(hipMemcpyAsync(uncompressed, ctx->out.p, size, hipMemcpyDeviceToHost, s));
+      SM_CHECK(hipStreamSynchronize(s));
+      *uncompressed_length = size;
+      return SM_OK;
+    }
+  }
+  ctx->last_path = 0;
   SM_CHECK(hipMemcpyAsync(d_off, &zero, 8, hipMemcpyHostToDevice, s));
   SM_CHECK(hipMemcpyAsync(d_in_len, hv, 8, hipMemcpyHostToDevice, s));
   sm::DecompressArgs a{(const uint8_t*)ctx->in.p, d_off, d_in_len, (uint8_t*)ctx->out.p, d_off, d_cap, d_out_len,

@@ -60,67 +60,6 @@ __device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N,
 }
 
 // ---------------------------------------------------------------------------------------
-// simple per-tag engine (streams declaring > 64 KiB, output in HBM)
-
-struct Window {
-  uint32_t w;
-  uint32_t base;
-};
-
-__device__ inline uint32_t win_ld32(const Window& win, uint32_t pos) {
-  uint32_t rel = pos - win.base;
-  uint32_t lo = readlane(win.w, rel >> 2);
-  uint32_t hi = readlane(win.w, (rel >> 2) + 1);
-  return __builtin_amdgcn_alignbyte(hi, lo, rel & 3);
-}
-
-__device__ int32_t decode_stream_global(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t size,
-                                        uint8_t* out, uint32_t lane) {
-  Window win;
-  win.w = load_word(in, N, ip + 4 * lane);
-  win.base = ip;
-  uint32_t op = 0;
-  volatile uint8_t* vo = out;
-  while ((int64_t)ip < (int64_t)N - 1) {                                 // internal.jl:416
-    if (ip - win.base > 4 * kWave - 8) {
-      win.w = load_word(in, N, ip + 4 * lane);
-      win.base = ip;
-    }
-    uint32_t c = win_ld32(win, ip) & 0xff;
-    uint32_t tag = win_ld32(win, ip + 1);                                // :426-430
-    ip += 1;
-    uint32_t entry = char_entry(c);                                      // :435-439
-    uint32_t len = entry & 0xff;
-    uint32_t taglen = entry >> 11;
-    uint32_t trailer = taglen >= 4 ? tag : (tag & ((1u << (8 * taglen)) - 1u));
-    ip += taglen;
-    if (c & 3) {                                                         // :458-460
-      uint32_t offset = (entry & 0x700) + trailer;
-      int64_t avail_out = (int64_t)size - op;
-      if ((int64_t)op <= (int64_t)(uint32_t)(offset - 1u)) return kErrCopyOffset;   // :499
-      if (!(len <= 16 && offset >= 8 && avail_out >= 16) && avail_out < (int64_t)len) return kErrCopyLength;
-      if (lane < len) {
-        uint32_t sidx = op - offset + (offset >= len ? lane : lane % offset);
-        vo[op + lane] = vo[sidx];
-      }
-      __threadfence_block();
-      op += len;
-    } else {                                                             // :461-462
-      uint32_t litlen = len + trailer;
-      int64_t avail_out = (int64_t)size - op;
-      int64_t avail_in = (int64_t)N - ip;
-      if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) return kErrLiteral;  // :518
-      for (uint32_t k = lane; k < litlen; k += kWave) vo[op + k] = in[ip + k];
-      __threadfence_block();
-      op += litlen;
-      ip += litlen;
-    }
-  }
-  if (op != size) return kErrInvalid;                                    // Snappy.jl:50
-  return kOk;
-}
-
-// ---------------------------------------------------------------------------------------
 // batched tag engine
 
 // size of a tag starting with byte c followed by `trailer` (u8; 255 = long literal)
@@ -247,8 +186,15 @@ __device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t from
   if (lane < to - from) out[from + lane] = win[(from + lane) & (kWin - 1)];
 }
 
-__device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t size,
-                                       uint8_t* out, uint8_t* ring, uint16_t* jt, uint8_t* win, uint32_t lane) {
+// Decodes the tags that start in [ip, ip_end) -- ip_end = N for a whole stream, whose loop
+// stops at N-1 (internal.jl:416) -- into out[op0, ...).  Copy sources below frag_lo are
+// refused with kErrCross: a fragment of a block-structured stream must not read output that
+// other waves produce (the caller then decodes the whole stream in order instead).  Error
+// checks use stream-global positions, so they are the reference's whatever the range.
+__device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t ip_end,
+                                       uint32_t size, uint8_t* out, uint32_t op0, uint32_t frag_lo, uint8_t* ring,
+                                       uint16_t* jt, uint8_t* win, uint32_t lane, uint32_t& op_end,
+                                       uint32_t op_lim = 0xffffffffu) {
   // ring holds stream bytes [wb, wb+768); pre1 = [wb+768, wb+1024) (loaded a batch ago),
   // pre2 = [wb+1024, wb+1280) issued at the end of the previous batch -- so a round's fence
   // (s_waitcnt vmcnt(0)) never waits for a freshly issued prefetch.
@@ -256,11 +202,11 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   uint32_t pre1, pre2;
   ring_fill(in, N, wb, ring, pre1, pre2, lane);
   bool issue_pre2 = false;
-  uint32_t op = 0, flushed = 0;  // output produced / already in HBM
-  const int64_t Nm1 = (int64_t)N - 1;
+  uint32_t op = op0, flushed = op0;  // output produced / already in HBM
+  const int64_t Nm1 = min((int64_t)N - 1, (int64_t)ip_end);  // parse limit
 
   STAMP_DECL
-  while ((int64_t)ip < Nm1) {
+  while ((int64_t)ip < Nm1 && op < op_lim) {
     STAMP_COUNT(6, 1)
     if (ip >= wb + 256) {
       if (ip < wb + 512) {
@@ -373,6 +319,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         const int64_t avail_out = (int64_t)size - (int64_t)opt;
         if (iscopy) {
           if ((int64_t)opt <= (int64_t)(uint32_t)(offset - 1u)) err = kErrCopyOffset;                    // :499
+          else if (opt - offset < frag_lo) err = kErrCross;
           else if (!(len <= 16 && offset >= 8 && avail_out >= 16) && avail_out < (int64_t)len) err = kErrCopyLength;  // :505
         } else {
           const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
@@ -381,10 +328,11 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
       const uint64_t em = ballot(err != kOk);
       if (em) return (int32_t)readlane((uint32_t)err, ctz64(em));
-      // cap the batch output at kBatchOut bytes (the window bound); one tag is <= 200 B
+      // cap the batch output at kBatchOut bytes (the window bound; one tag is <= 200 B) and at
+      // the output limit (a fragment ends where the next one starts)
       uint32_t nt = ntok;
-      if (readlane(incl, ntok - 1) > kBatchOut) {
-        nt = (uint32_t)__builtin_popcountll(ballot(mine && incl <= kBatchOut));
+      if (readlane(incl, ntok - 1) > kBatchOut || readlane(opt, ntok - 1) >= op_lim) {
+        nt = (uint32_t)__builtin_popcountll(ballot(mine && incl <= kBatchOut && opt < op_lim));
         ipw = ip + readlane(tnext, nt - 1);
         big = false;  // the next tag is a batch tag inside the window
       }
@@ -518,6 +466,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
       STAMP(4)
       op += X;
+      if (op > op_lim) return kErrCross;  // a tag crosses the fragment end
       win_flush(out, win, flushed, op & ~15u, lane);  // whole 16-byte blocks to HBM
       flushed = max(flushed, op & ~15u);
       ip = ipw;
@@ -527,7 +476,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       issue_pre2 = false;
     }
 
-    if (big) {
+    if (big && op < op_lim) {  // (at op_lim the literal opens the next fragment)
       // one literal too long for the batch path (or a wrapped length): straight to HBM
       const uint64_t hv = ring_get8(ring, ip);
       const uint32_t c = uniform((uint32_t)hv & 0xff);
@@ -540,6 +489,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const int64_t avail_out = (int64_t)size - (int64_t)op;
       const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
       if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) return kErrLiteral;  // :518
+      if ((uint64_t)op + litlen > op_lim) return kErrCross;
       win_flush(out, win, flushed, op, lane);  // HBM holds everything before the literal
       // bulk copy: head bytes to 16-B source alignment, then 16 B per lane, 4 in flight
       const uint8_t* s = in + lsrc;
@@ -591,7 +541,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   win_flush(out, win, flushed, op, lane);
   STAMP(5)
   STAMP_FLUSH(g_stamp)
-  if (op != size) return kErrInvalid;                                    // Snappy.jl:50
+  op_end = op;
   return kOk;
 }
 
@@ -630,16 +580,152 @@ __global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
   }
   if (st == kOk && size > cap) st = kBufferTooSmall;
   if (st == kOk) {
-    if (size <= kBlockSize) {
-      st = decode_stream_batch(in, N, ip, size, dst, sring, sjt, swin, lane);
-    } else {
-      st = decode_stream_global(in, N, ip, size, dst, lane);
-    }
+    uint32_t op_end = 0;
+    st = decode_stream_batch(in, N, ip, N, size, dst, 0, 0, sring, sjt, swin, lane, op_end);
+    if (st == kOk && op_end != size) st = kErrInvalid;                                    // Snappy.jl:50
   }
   if (lane == 0) {
     a.status[b] = st;
     a.out_len[b] = st == kOk ? size : 0;
   }
+}
+
+// ---- one large stream, decoded in parallel ------------------------
+// Snappy.jl (src/Snappy.jl:29-33), libsnappy and this library compress 64 KiB blocks
+// independently, so in their streams every output multiple of 65536 is a tag start and no copy
+// reaches into an earlier block.  Finding those tags needs the tag boundaries, which the format
+// does not index:
+//  1. k_stream_index, one wave per 4 KiB chunk of the compressed body: lane 0 walks the tags
+//     speculatively from the chunk's first byte, recording each visited position and the output
+//     before it; lanes l = 1..63 walk from byte l until they meet lane 0's path (tag walks
+//     resynchronise within a few tags on compressible data) or leave the chunk.  Each chunk then
+//     knows, for entry offsets 0..63, where the walk leaves it and how much output it makes.
+//  2. The host chains the true path (sm_api.hip) and locates each fragment's chunk.
+//  3. k_decompress_frags, one wave per fragment: walk from the chunk entry to the tag at output
+//     F, then the batch engine with frag_lo = F and the output limit F + 65536.
+// Anything unexpected (kErrCross, an error, a length mismatch) sends the caller to the in-order
+// decode, which reproduces the reference's accept/reject exactly.
+
+// stream tag at byte rel of an LDS copy: its size in the stream and its output bytes
+// (char_entry / zero-padded lookahead: internal.jl:426-462)
+__device__ inline void tag_at(const uint8_t* buf, uint32_t rel, uint64_t& size, uint64_t& outb) {
+  const uint64_t hv = lds_ld64(buf, rel);
+  const uint32_t c = (uint32_t)hv & 0xff;
+  const uint32_t entry = char_entry(c);
+  const uint32_t taglen = entry >> 11;
+  const uint32_t tr_raw = (uint32_t)(hv >> 8);
+  const uint32_t trailer = taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * taglen)) - 1u));
+  if (c & 3) {
+    size = 1 + taglen;
+    outb = entry & 0xff;
+  } else {
+    const uint32_t lit = (entry & 0xff) + trailer;  // u32 wrap, as the reference
+    size = 1ull + taglen + lit;
+    outb = lit;
+  }
+}
+
+// bytes [s, s+len) of the stream into LDS, zero past N (the reference's zero-padded lookahead)
+__device__ inline void stage_bytes(uint8_t* buf, const uint8_t* __restrict__ in, uint32_t N, uint32_t s, uint32_t len,
+                                   uint32_t lane) {
+  for (uint32_t k = lane; k < len; k += kWave) buf[k] = s + k < N ? in[s + k] : 0;
+}
+
+__global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
+                                                     uint32_t* rec_exit, uint32_t* rec_out) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kIdxChunk + 16];
+  __shared__ uint32_t bm[kIdxChunk / 32];  // positions on lane 0's path
+  __shared__ uint32_t cum[kIdxChunk];      // output before each such position
+  const uint32_t c = blockIdx.x, lane = lane_id();
+  const uint32_t s = ip0 + c * kIdxChunk;
+  stage_bytes(buf, in, N, s, kIdxChunk + 16, lane);
+  for (uint32_t k = lane; k < kIdxChunk / 32; k += kWave) bm[k] = 0;
+  __syncthreads();
+  const uint64_t lim = min((uint64_t)s + kIdxChunk, (uint64_t)N - 1);  // tags start below N-1 (:416)
+  uint64_t p = s, acc = 0, size, outb;
+  while (p < lim) {  // lane 0's path, wave-uniform
+    const uint32_t rel = (uint32_t)(p - s);
+    if (lane == 0) {
+      bm[rel >> 5] |= 1u << (rel & 31);
+      cum[rel] = (uint32_t)acc;
+    }
+    tag_at(buf, rel, size, outb);
+    acc += outb;
+    p += size;
+  }
+  __syncthreads();
+  const uint64_t exit0 = p;
+  const uint32_t tot0 = (uint32_t)acc;
+  uint64_t q = (uint64_t)s + lane, ex = exit0;
+  uint32_t pre = 0, res = tot0;
+  bool done = lane == 0;
+  while (ballot(!done)) {
+    if (!done) {
+      if (q >= lim) {
+        ex = q;
+        res = pre;
+        done = true;
+      } else {
+        const uint32_t rel = (uint32_t)(q - s);
+        if ((bm[rel >> 5] >> (rel & 31)) & 1u) {  // met lane 0's path
+          ex = exit0;
+          res = pre + (tot0 - cum[rel]);
+          done = true;
+        } else {
+          tag_at(buf, rel, size, outb);
+          pre += (uint32_t)outb;
+          q += size;
+        }
+      }
+    }
+  }
+  rec_exit[c * kIdxEntries + lane] = (uint32_t)min(ex, (uint64_t)0xffffffffu);
+  rec_out[c * kIdxEntries + lane] = res;
+}
+
+__global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
+                                                            uint8_t* out, const StreamFrag* frags, int32_t* status) {
+  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[kWalkLevels * 256];
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf[kIdxChunk + 32];
+  const uint32_t f = blockIdx.x, lane = lane_id();
+  const StreamFrag fr = frags[f];
+  // walk from the chunk entry to the tag that starts at output F (inside that chunk)
+  stage_bytes(sbuf, in, N, fr.y, kIdxChunk + 32, lane);
+  __syncthreads();
+  uint64_t p = fr.y, o = fr.O, tsz, outb;
+  int32_t st = kOk;
+  while (o < fr.F) {
+    if (p - fr.y >= kIdxChunk + 16) {
+      st = kErrCross;
+      break;
+    }
+    tag_at(sbuf, (uint32_t)(p - fr.y), tsz, outb);
+    o += outb;
+    p += tsz;
+  }
+  if (st == kOk && o != fr.F) st = kErrCross;  // no tag starts at F: not block-structured
+  if (st == kOk) {
+    uint32_t op_end = 0;
+    st = decode_stream_batch(in, N, (uint32_t)p, N, size, out, fr.F, fr.F, sring, sjt, swin, lane, op_end, fr.lim);
+    if (st == kOk && op_end != (fr.lim == 0xffffffffu ? size : fr.lim)) st = kErrCross;
+  }
+  if (lane == 0) status[f] = st;
+}
+
+hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec_exit,
+                               uint32_t* rec_out, hipStream_t s) {
+  if (nchunks == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_stream_index, dim3(nchunks), dim3(64), 0, s, in, N, ip0, rec_exit, rec_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_decompress_frags(const uint8_t* in, uint32_t N, uint32_t size, uint8_t* out,
+                                   const StreamFrag* frags, uint32_t nfrag, int32_t* status, hipStream_t s) {
+  if (nfrag == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_decompress_frags, dim3(nfrag), dim3(64), 0, s, in, N, size, out, frags, status);
+  return hipGetLastError();
 }
 
 hipError_t launch_decompress(const DecompressArgs& a, int /*large*/, hipStream_t s) {

@@ -53,6 +53,7 @@ enum : int32_t {
   kErrCopyOffset = 19,
   kErrCopyLength = 20,
   kErrLiteral = 21,
+  kErrCross = 64,  // internal: a fragment's copy reads another fragment (never returned by the ABI)
 };
 
 __host__ __device__ inline uint32_t max_compressed_length(uint32_t n) { return 32 + n + n / 6; }

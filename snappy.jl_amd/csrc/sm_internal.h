@@ -36,6 +36,21 @@ struct DecompressArgs {
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s);
 hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s);
 hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
+
+// One large stream decoded in parallel (sm_uncompress): an index pass over 4 KiB chunks of the
+// compressed body, then one wave per 64 KiB output fragment (see sm_decompress.hip).
+constexpr uint32_t kIdxChunk = 4096;  // compressed bytes per index chunk
+constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
+struct StreamFrag {
+  uint32_t y;    // a true tag start at or before the fragment's first tag (chunk entry)
+  uint32_t O;    // output position of the tag at y
+  uint32_t F;    // the fragment's first output position (a multiple of 65536)
+  uint32_t lim;  // output limit (0xffffffff for the last fragment: parse to the end)
+};
+hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec_exit,
+                               uint32_t* rec_out, hipStream_t s);
+hipError_t launch_decompress_frags(const uint8_t* in, uint32_t N, uint32_t size, uint8_t* out,
+                                   const StreamFrag* frags, uint32_t nfrag, int32_t* status, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)
 hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
                          const uint64_t* dst_off, uint8_t* dst, uint32_t nblk, hipStream_t s);

@@ -274,3 +274,52 @@ def test_decompress_random_op_streams(sm, gpu_available):
     outs = _decode_all(sm, [s for s, _ in built])
     for (s, expect), o in zip(built, outs):
         assert o == expect
+
+
+# ---- one large stream: parallel fragment decode (sm_uncompress) ---------------------------
+
+def _big_corpus(n):
+    raw = b"".join(read_testfile(f) for f in sorted(GOLDEN["corpus"]))
+    return (raw * (n // len(raw) + 1))[:n]
+
+
+def test_uncompress_large_stream_parallel(sm, oracle, libsnappy, gpu_available):
+    """Block-structured streams (Snappy.jl = oracle, libsnappy, this library's fast mode) of
+    more than 4 fragments decode through the parallel fragment path, bit-exactly."""
+    raw = _big_corpus(1_500_000)
+    rng = np.random.default_rng(9)
+    noise = rng.integers(0, 256, 1_000_000, dtype=np.uint8).tobytes()
+    mixed = b"".join(raw[i:i + 50_000] + noise[i:i + 30_000] for i in range(0, 900_000, 80_000))
+    # every 64 KiB block starting with a long literal (> 200 B: the batch path's big literals)
+    blocky = b"".join(noise[i * 1000:i * 1000 + 700] + raw[i * 65536:i * 65536 + 64836] for i in range(8))
+    for data in (raw, noise, mixed, blocky):
+        for comp in (oracle.compress(data), libsnappy.compress(data), sm.compress(data, mode="fast")):
+            assert sm.uncompress(comp) == data
+            assert sm.last_uncompress_path() == 1
+
+
+def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
+    """Valid streams that are not block-structured (copies into earlier 64 KiB blocks, a
+    literal across a fragment start) and corrupted large streams take the in-order decode,
+    with the oracle's output and status."""
+    from streams import build, random_ops
+    rng = np.random.default_rng(31)
+    s1, e1 = build(random_ops(rng, 400_000))                        # offsets up to 65535
+    s2, e2 = build([("lit", rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes())] +
+                   [("copy", 1000, 64)] * 5000)                      # literal across 65536
+    for s, e in ((s1, e1), (s2, e2)):
+        assert sm.uncompress(s) == e
+        assert sm.last_uncompress_path() == 0
+    good = oracle.compress(_big_corpus(600_000))
+    for i in range(40):
+        bad = bytearray(good)
+        for _ in range(int(rng.integers(1, 4))):
+            bad[int(rng.integers(5, len(bad)))] = int(rng.integers(0, 256))
+        st_o, out_o = oracle.uncompress_status(bytes(bad))
+        try:
+            st_g, out_g = 0, sm.uncompress(bytes(bad))
+        except sm.SnappyError as exc:
+            st_g, out_g = exc.code, None
+        assert st_g == st_o
+        if st_o == 0:
+            assert out_g == out_o
