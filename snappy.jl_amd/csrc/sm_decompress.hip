@@ -229,66 +229,48 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     // Parallel tag walk by pointer doubling over the 256 window positions (VALU + LDS, no
     // serial SALU loop).  J0[p] = p + size(p); a position whose tag is a long literal, or that
     // lies at/after the parse limit (window end or N-1, internal.jl:416), is a stop node
-    // (J0[p] = p, self-loop).  J_k = J_{k-1} o J_{k-1}, k < kWalkLevels: a batch takes at most
-    // 64 tags, i.e. chain elements 0..63 steps from the window's first position (ip), and the
-    // binary descent from 0 along J_5..J_0 (largest chain element <= p within 63 steps) lands
-    // on p iff p is one of them.
+    // (J0[p] = p, self-loop).  J_k = J_{k-1} o J_{k-1}, k < kWalkLevels (a batch takes at most
+    // 64 tags, chain elements 0..63 steps from the window's first position, ip).
     const uint32_t wlim = (int64_t)(ip + 256) < Nm1 ? ip + 256 : (uint32_t)Nm1;
     const uint32_t rlim = wlim - ip;
-    uint32_t J[4], nxt[4];
-    bool stopn[4];
+    uint32_t J[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint32_t p = 4 * lane + j;
       const uint32_t sz = (sizes >> (8 * j)) & 0xff;
-      stopn[j] = sz == 255 || p >= rlim;
-      nxt[j] = p + sz;
-      J[j] = stopn[j] ? p : p + sz;
+      J[j] = (sz == 255 || p >= rlim) ? p : p + sz;
     }
     uint16_t* jt0 = jt;
     *reinterpret_cast<uint2*>(jt0 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
 #pragma unroll
     for (int k = 1; k < kWalkLevels; ++k) {
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
       const uint16_t* prev = jt + (k - 1) * 256;
 #pragma unroll
       for (int j = 0; j < 4; ++j) J[j] = J[j] < 256 ? prev[J[j]] : J[j];
       *reinterpret_cast<uint2*>(jt + k * 256 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
     }
-    uint32_t cur[4] = {0, 0, 0, 0};
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the u16 reads below follow the uint2 stores
+    // Tag t of the batch sits in lane t: apply J_k for every set bit k of t to position 0
+    // (chain element t).  Stop nodes are fixed points, so the lanes past the batch's last tag
+    // all land on the first stop (or beyond the window) -- the tags are a prefix of lanes.
+    uint32_t cpos = 0;
 #pragma unroll
-    for (int k = kWalkLevels - 1; k >= 0; --k) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint32_t t = jt[k * 256 + cur[j]];
-        cur[j] = t <= 4 * lane + j ? t : cur[j];
-      }
+    for (int k = 0; k < kWalkLevels; ++k) {
+      const uint32_t t = cpos < 256 ? jt[k * 256 + cpos] : cpos;
+      cpos = ((lane >> k) & 1u) ? t : cpos;
     }
-    bool isv[4];
-    uint32_t cnt = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t p = 4 * lane + j;
-      isv[j] = cur[j] == p && !stopn[j];  // a tag of this batch
-      cnt += isv[j] ? 1u : 0u;
-    }
-    const uint32_t rank0 = scan_dpp(cnt) - cnt;
-    const uint32_t nvalid = readlane(rank0 + cnt, 63);
-    // compact: slot[rank] = p | next << 16 (slots 0..63; reuses jt level 0, no longer read)
-    {
-      uint32_t rk = rank0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (isv[j] && rk < 64) reinterpret_cast<uint32_t*>(jt)[rk] = (4 * lane + j) | (nxt[j] << 16);
-        rk += isv[j] ? 1u : 0u;
-      }
-    }
-    const uint32_t ntok = nvalid < 64 ? nvalid : 64;
+    // (the shuffle runs with every lane active: a ds_bpermute from an inactive lane reads 0)
+    const uint32_t szw = __shfl(sizes, (cpos >> 2) & 63u, 64);
+    const uint32_t csz = cpos < 256 ? (szw >> (8 * (cpos & 3))) & 0xffu : 0u;
+    const bool ctag = cpos < rlim && csz != 255;  // rlim <= 256
+    const uint64_t tm = ballot(ctag);
+    const uint32_t ntok = (uint32_t)__builtin_popcountll(tm);
     uint32_t tpos = 0, ipw = ip, tnext = 0;
     bool big = false;
     if (ntok) {
-      const uint32_t sv = reinterpret_cast<const uint32_t*>(jt)[lane < ntok ? lane : 0];
-      tpos = ip + (sv & 0xffff);
-      tnext = sv >> 16;
+      tpos = ip + cpos;
+      tnext = cpos + csz;
       ipw = ip + readlane(tnext, ntok - 1);
     }
     if (ipw < wlim) {
