@@ -140,12 +140,16 @@ constexpr uint32_t kWin = 4096;
 constexpr uint32_t kBatchOut = 1024;
 constexpr uint32_t kLdsSrc = kWin - kBatchOut - 64;
 
-__device__ inline uint64_t win_get8(const uint8_t* win, uint32_t x) {
-  const uint64_t* w = reinterpret_cast<const uint64_t*>(win);
-  const uint32_t sl = x & (kWin - 1), i = sl >> 3, sh = 8 * (sl & 7);
-  const uint64_t lo = w[i], hi = w[(i + 1) & (kWin / 8 - 1)];
+// 8 bytes at byte x of an LDS ring of msk+1 bytes (power of 2, 8-aligned base): two aligned
+// ds_read_b64 and a funnel shift, the ring wrapping by index
+__device__ inline uint64_t lds_get8w(const uint8_t* bb, uint32_t msk, uint32_t x) {
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(bb);
+  const uint32_t sl = x & msk, i = sl >> 3, sh = 8 * (sl & 7);
+  const uint64_t lo = w[i], hi = w[(i + 1) & (msk >> 3)];
   return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
 }
+
+__device__ inline uint64_t win_get8(const uint8_t* win, uint32_t x) { return lds_get8w(win, kWin - 1, x); }
 
 // OR the low cnt (1..8) bytes of v into the (zeroed) window at output position x
 __device__ inline void win_put8(uint8_t* win, uint32_t x, uint64_t v, uint32_t cnt) {
@@ -376,29 +380,31 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
           if (!ballot(act)) break;
           if (act) {
             uint64_t v[kPass];
-            if (!iscopy) {
-#pragma unroll
-              for (int i = 0; i < kPass; ++i)
-                v[i] = base + 8 * i < L ? ring_get8(ring, lsrc + base + 8 * i) : 0ull;
-            } else if (offset >= 8) {
-              const uint64_t B = gsrc ? *reinterpret_cast<const du64u*>(out + slo) : win_get8(win, slo);
+            if (!iscopy || offset >= 8) {
+              // a literal (input ring; it never wraps) or a copy with offset >= 8 (output window,
+              // or HBM for far sources): 8-byte pieces of S, wrapping once to S's start
+              const uint8_t* bb = iscopy ? win : ring;
+              const uint32_t msk = iscopy ? kWin - 1 : kRing - 1;
+              const uint32_t sp = iscopy ? slo : lsrc;
+              const uint32_t off = iscopy ? offset : 0xffffu;
+              const uint64_t B = gsrc ? *reinterpret_cast<const du64u*>(out + slo) : lds_get8w(bb, msk, sp);
               uint32_t m0 = base;
-              while (m0 >= offset) m0 -= offset;
+              while (m0 >= off) m0 -= off;
               uint32_t m = m0;
 #pragma unroll
               for (int i = 0; i < kPass; ++i) {
-                v[i] = base + 8 * i < L ? (gsrc ? *reinterpret_cast<const du64u*>(out + slo + m) : win_get8(win, slo + m))
+                v[i] = base + 8 * i < L ? (gsrc ? *reinterpret_cast<const du64u*>(out + slo + m) : lds_get8w(bb, msk, sp + m))
                                         : 0ull;
                 m += 8;
-                if (m >= offset) m -= offset;
+                if (m >= off) m -= off;
               }
               m = m0;
 #pragma unroll
               for (int i = 0; i < kPass; ++i) {
-                const uint32_t keep = offset - m;  // bytes of this chunk before S wraps
+                const uint32_t keep = off - m;  // bytes of this chunk before S wraps
                 if (keep < 8) v[i] = (v[i] & ((1ull << (8 * keep)) - 1)) | (B << (8 * keep));
                 m += 8;
-                if (m >= offset) m -= offset;
+                if (m >= off) m -= off;
               }
             } else {
               const uint64_t x = win_get8(win, slo);

@@ -20,7 +20,7 @@ static uint32_t copy_bytes(uint32_t off, uint32_t len) {
 
 // policy: 0 = first-chance only (prior rounds), 1 = second chance else first, 2 = best of both,
 //         3 = exact latest-earlier (ideal table)
-static int g_nbr = 0, g_first = 0, g_skip = 0;  // probe the private tables of g_nbr previous chunks
+static int g_nbr = 0, g_first = 0, g_skip = 0, g_nonempty = 0;  // probe the private tables of g_nbr previous chunks
 
 static uint64_t model_block(const uint8_t* d, uint32_t n, uint32_t chunk, uint32_t waves, uint32_t tab,
                             int policy, int exact_intrachunk) {
@@ -71,6 +71,11 @@ static uint64_t model_block(const uint8_t* d, uint32_t n, uint32_t chunk, uint32
             if (cands[i] && cands[i] - 1 < p && ld32(d + cands[i] - 1) == ld32(d + p)) have = 1;
           for (int m = 1; m <= g_nbr && !(g_skip && have) && (int)(k - r * waves) - m >= 0; ++m) {
             uint32_t v = P[k - r * waves - m][(ld32(d + p) * 0x1e35a7bdu) >> 24];
+            if (g_nonempty) {  // take the nearest non-empty entry, verified or not
+              if (!v) continue;
+              nb[nn++] = v;
+              break;
+            }
             if (g_first && !(v && v - 1 < p && ld32(d + v - 1) == ld32(d + p))) continue;
             nb[nn++] = v;
             if (g_first) break;
@@ -108,6 +113,7 @@ int main(int argc, char** argv) {
   if (getenv("NBR")) g_nbr = atoi(getenv("NBR"));  // e.g. NBR=4 FIRST=1 (nearest verified only)
   if (getenv("FIRST")) g_first = 1;
   if (getenv("SKIP")) g_skip = 1;                   // probe only positions without a verified A/B
+  if (getenv("NONEMPTY")) g_nonempty = 1;           // nearest non-empty neighbour entry only
   struct { uint32_t chunk, waves, tab; int pol, intra; } cfg[] = {
       {256, 4, 16384, 2, 1}, {256, 8, 16384, 2, 1}, {128, 8, 16384, 2, 1}, {256, 8, 16384, 1, 1},
       {256, 4, 12288, 2, 1}, {256, 8, 12288, 2, 1}, {256, 4, 8192, 2, 1}, {256, 8, 8192, 2, 1},
