@@ -281,11 +281,11 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       // Greedy parse by pointer doubling (no serial loop) over the chunk's 128 positions.
       // J0 skips literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a
       // non-match), else the chunk end, so the greedy walk from 0 steps only between copies
-      // (<= 32 copies of >= 4 bytes: 31 steps); J_k = J_{k-1} o J_{k-1}.  Position r is
-      // visited iff the binary descent along J_4..J_0 (largest visited position <= r) lands
-      // on r; visited match positions are the copies.
-      uint32_t cur[2] = {0xffffu, 0xffffu};  // no copies at all (incompressible): skip the parse
+      // (<= 32 copies of >= 4 bytes: 31 steps); J_k = J_{k-1} o J_{k-1}, k < 5.  Copy t of the
+      // chunk is then computed directly in lane t from the jump tables.
+      // no copies at all (incompressible): skip the parse
       const uint64_t M0 = ballot(Ls[0] != 0), M1 = ballot(Ls[1] != 0);
+      uint32_t nmatch = 0, last_end = 0;
       if (M0 | M1) {
         uint32_t jv[2];
 #pragma unroll
@@ -300,47 +300,49 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         }
 #pragma unroll
         for (int k = 1; k < (int)kLevels; ++k) {
+          __atomic_signal_fence(__ATOMIC_SEQ_CST);
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
             jv[j] = jv[j] < kChunk ? jt[(k - 1) * kChunk + jv[j]] : jv[j];
             jt[k * kChunk + 64 * j + lane] = (uint8_t)jv[j];
           }
         }
-        cur[0] = cur[1] = 0;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        // chain element t (lane t < 32) from position 0: J_k for every set bit k of t.  Only
+        // element 0 can be a non-match (J0 jumps to match positions), the rest are the copies.
+        uint32_t c = 0;
 #pragma unroll
-        for (int k = kLevels - 1; k >= 0; --k) {
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const uint32_t t = jt[k * kChunk + cur[j]];
-            cur[j] = t <= 64u * j + lane ? t : cur[j];
-          }
+        for (int k = 0; k < (int)kLevels; ++k) {
+          const uint32_t t = c < kChunk ? jt[k * kChunk + c] : c;
+          c = ((lane >> k) & 1u) ? t : c;
         }
+        // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles
+        const uint32_t ci = c & 63u;
+        const uint32_t l0 = __shfl(Ls[0], ci, 64), l1 = __shfl(Ls[1], ci, 64);
+        const uint32_t o0 = __shfl(offs[0], ci, 64), o1 = __shfl(offs[1], ci, 64);
+        const uint32_t Lc = c < 64 ? l0 : (c < kChunk ? l1 : 0u);
+        const uint32_t oc = c < 64 ? o0 : o1;
+        const bool istok = lane < 32 && Lc != 0;
+        const uint64_t tm = ballot(istok);
+        nmatch = (uint32_t)__builtin_popcountll(tm);
+        const uint32_t sh = (uint32_t)(tm & 1u) ^ 1u;  // tokens start at lane 1 if 0 is no match
+        const uint32_t tav = __shfl(c | (Lc << 16), lane + sh, 64), tbv = __shfl(oc, lane + sh, 64);
+        if (nmatch) {
+          ta = tav;
+          tb = tbv;
+          last_end = readlane(c + Lc, nmatch - 1 + sh);
+        }
+        // copy-start bitmask (position p of the chunk) for the literal scatter
+        uint64_t* tsw = reinterpret_cast<uint64_t*>(jt);
+        if (lane == 0) tsw[0] = tsw[1] = 0;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (istok)
+          __hip_atomic_fetch_or(&tsw[c >> 6], 1ull << (c & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        ts0 = tsw[0];
+        ts1 = tsw[1];
       }
       STAMP(4)
-      const bool tok0 = cur[0] == lane && Ls[0] != 0;
-      const bool tok1 = cur[1] == 64 + lane && Ls[1] != 0;
-      ts0 = ballot(tok0);
-      ts1 = ballot(tok1);
-      const uint32_t n0 = __builtin_popcountll(ts0);
-      const uint32_t nmatch = n0 + __builtin_popcountll(ts1);
-      uint32_t last_end = 0;
-      if (nmatch) {  // end of the last copy (highest token position)
-        const uint32_t j = ts1 ? 1u : 0u;
-        const uint64_t m = ts1 ? ts1 : ts0;
-        const uint32_t l = 63 - (uint32_t)__builtin_clzll(m);
-        last_end = 64 * j + l + readlane(j ? Ls[1] : Ls[0], l);
-      }
-      // compact the copies into lanes 0..nmatch-1 (slots reuse J levels 0..4, no longer read)
-      uint2* slots = reinterpret_cast<uint2*>(jt);
-      if (tok0) slots[__builtin_amdgcn_mbcnt_hi((uint32_t)(ts0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ts0, 0u))] =
-          make_uint2(lane | (Ls[0] << 16), offs[0]);
-      if (tok1) slots[n0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(ts1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ts1, 0u))] =
-          make_uint2((64 + lane) | (Ls[1] << 16), offs[1]);
-      if (lane < nmatch) {
-        const uint2 sv = slots[lane];
-        ta = sv.x;
-        tb = sv.y;
-      }
       ntok = nmatch;
       if (last_end < ce - c0) {  // trailing literal run: a token without a copy
         const bool me = lane == ntok;
@@ -480,7 +482,6 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 constexpr size_t kFastLds =
     kBlockSize + 4 * (kFTab + kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * kLevels * kChunk;
 static_assert(kFastLds <= 160 * 1024, "fast compressor LDS exceeds a CU");
-static_assert(65 * sizeof(uint2) <= kLevels * kChunk, "token slots overflow the jump tables");
 
 hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s) {
   static bool attr_set = false;
