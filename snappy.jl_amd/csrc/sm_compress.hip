@@ -19,6 +19,11 @@
 
 namespace sm {
 
+#if SM_STAMP
+__device__ unsigned long long g_stamp_x[8];
+#endif
+STAMP_MACROS(8)
+
 constexpr uint32_t kLdsPad = 64;  // readable slack after the block for lds_ld32 / wave compares
 
 // ---- output emission (global memory, wave-uniform op) -------------------------------
@@ -133,8 +138,10 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
   const int32_t ip_limit = (int32_t)n - 16;  // internal.jl:131, Q1: 1-based ip_end-15
   uint32_t ip = 0, next_emit = 0, cand = 0;
 
+  STAMP_DECL
   if (n >= kInputMarginBytes) {                                                // internal.jl:133
     for (;;) {
+      STAMP(4)
       ip += 1;                                                                 // :163
       // literal search, 64 probes per step (:167-194)
       const uint32_t p0 = ip;
@@ -160,11 +167,15 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         }
         if (ballot(valid) != ~0ull) break;                                     // :175 -> remainder
       }
+      STAMP(0)
       if (!found) goto emit_remainder;
       op = emit_literal_g(dst, op, sdata, next_emit, ip - next_emit, lane, true);   // :200
+      STAMP(1)
       for (;;) {                                                               // :211-239
+        STAMP_COUNT(6, 1)
         uint32_t avail = e - (ip + 4) + 1;
         uint32_t matched = 4 + wave_match_length(sdata, cand + 4, ip + 4, avail, lane);  // :216
+        STAMP(2)
         op = emit_copy_g(dst, op, ip - cand, matched, lane);                   // :217
         ip += matched;
         next_emit = ip;
@@ -176,12 +187,18 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         const uint32_t rv = uniform(stab[cur_hash]);                           // :234
         cand = rv ? rv - 1 : 0u;
         if (lane == 0) stab[cur_hash] = ip + 1;                                // :235 (pos ip)
-        if (input_bytes != uld32(sdata, cand)) break;                          // :238
+        if (input_bytes != uld32(sdata, cand)) {                               // :238
+          STAMP(3)
+          break;
+        }
+        STAMP(3)
       }
     }
   }
 emit_remainder:
   if (next_emit <= e) op = emit_literal_g(dst, op, sdata, next_emit, e - next_emit + 1, lane, true);  // :244-248
+  STAMP(5)
+  STAMP_FLUSH(g_stamp_x)
   if (lane == 0) a.out_len[b] = op;
 }
 
@@ -196,6 +213,17 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ src,
   const uint32_t n = len[b];
   for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) d[k] = s[k];
 }
+
+#if SM_STAMP
+extern "C" int sm_debug_stamps_x(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_x), sizeof(g_stamp_x)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[8] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_x), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s) {
   if (a.nblk == 0) return hipSuccess;

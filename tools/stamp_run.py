@@ -30,10 +30,12 @@ def main():
     ap.add_argument("--blocks", type=int, default=4000)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--data", default="text")
-    ap.add_argument("--op", default="uncompress", choices=["uncompress", "compress_fast"])
+    ap.add_argument("--op", default="uncompress", choices=["uncompress", "compress_fast", "compress_ref"])
     args = ap.parse_args()
     if args.op == "compress_fast":
         return compress_stamps(args)
+    if args.op == "compress_ref":
+        return exact_stamps(args)
     sm = bench.load_package()
     lib = sm.lib()
     fn = lib.sm_debug_stamps
@@ -83,6 +85,31 @@ def compress_stamps(args):
     for i, nme in enumerate(CNAMES):
         print("  %-14s %5.1f%%  %7.0f cycles/wave-round" % (nme, 100.0 * v[i] / tot, v[i] / max(rounds, 1)))
     print("  total          %7.0f cycles/wave-round" % (tot / max(rounds, 1)))
+
+
+XNAMES = ["search", "literal emit", "match length", "emit+hash+table+verify", "loop top", "remainder"]
+
+
+def exact_stamps(args):
+    sm = bench.load_package()
+    fn = sm.lib().sm_debug_stamps_x
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    dev = torch.device("cuda", 0)
+    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 7)
+    b = bench.Batch(blocks, dev)
+    buf = (ctypes.c_ulonglong * 8)()
+    b.compress(sm, "reference")
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    b.compress(sm, "reference")
+    torch.cuda.synchronize()
+    fn(buf, 1)
+    v = list(buf)
+    copies = v[6]
+    tot = sum(v[:6])
+    print("compress_ref %s: %d copy steps (%.0f per block)" % (args.data, copies, copies / args.blocks))
+    for i, nme in enumerate(XNAMES):
+        print("  %-24s %5.1f%%  %7.0f cycles/copy" % (nme, 100.0 * v[i] / tot, v[i] / max(copies, 1)))
 
 
 if __name__ == "__main__":
