@@ -327,22 +327,10 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       STAMP(2)
 
       win_zero(win, op, X, lane);
-      // dependencies: tfirst = last tag u < t whose output starts at or before the source start
       const uint32_t O0 = op;
       const uint32_t slo = opt - offset;
       const uint32_t shi = slo + min(len, offset);
       const bool gsrc = iscopy && offset > kLdsSrc;  // source older than the window: from HBM
-      uint32_t lo = 0, hi = lane ? lane - 1 : 0;
-#pragma unroll
-      for (int it = 0; it < 6; ++it) {
-        const uint32_t mid = (lo + hi + 1) >> 1;
-        const uint32_t om = __shfl(opt, mid, 64);
-        if (lo < hi) {
-          if (om <= slo) lo = mid;
-          else hi = mid - 1;
-        }
-      }
-      const uint32_t tfirst = lo;
       const uint64_t all = nt == 64 ? ~0ull : ((1ull << nt) - 1);
       const bool longlit = !iscopy && litlen > 64;
       uint64_t done = (ballot(longlit) & all) | ~all;
@@ -360,19 +348,17 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
 
       STAMP(3)
-      // One round (all in LDS) runs every tag whose source is final before the batch (or only
-      // needs the long literals above); its writes never touch bytes another ready tag reads:
+      // One round (all in LDS) runs every tag whose source is final before the batch; its
+      // writes never touch bytes another ready tag reads:
       //  * literal (<= 64 B): 8-byte pieces of the input ring;
       //  * copy: its source window S = out[slo, slo+offset) is final when the round starts, and
       //    output byte j is S[j mod offset] (incremental_copy_slow!, internal.jl:477-481), so
       //    chunk i = S from phase m = 8i mod offset, wrapping once to S's start (offset >= 8);
       //    for offset < 8 the period is unrolled to 16 bytes in registers.
-      const uint64_t range = lane > tfirst ? (((1ull << lane) - 1) & ~((1ull << tfirst) - 1)) : 0ull;
       if (SM_ABLATE_D & 1) done = ~0ull;
       if (done != ~0ull) {
         STAMP_COUNT(7, 1)
-        const bool ready = !((done >> lane) & 1) &&
-                           ((SM_ABLATE_D & 2) || !iscopy || shi <= O0 || ((~done) & range) == 0);
+        const bool ready = !((done >> lane) & 1) && ((SM_ABLATE_D & 2) || !iscopy || shi <= O0);
         const uint64_t rm = ballot(ready);
         const uint32_t L = iscopy ? len : litlen;
         for (uint32_t base = 0; base < 64; base += 8 * kPass) {
