@@ -6,14 +6,14 @@
 //
 // One workgroup of W = 16 waves per block (four per SIMD, to hide the chain of LDS round
 // trips); the block is staged once in LDS (64 KiB) beside a shared 16 K-entry latest-position
-// table (u32, 64 KiB), a 256-entry private table per wave (16 KiB) and 5-level parse jump
+// table (u32, 64 KiB), a 128-entry u64 private table per wave (16 KiB) and 5-level parse jump
 // tables (10 KiB): 154 KiB, one block per CU.  The block is cut into 128-byte chunks whose
 // parse never crosses the chunk end (copies are truncated there, literal runs end there), so
 // the chunks of a round are parsed independently: in round r wave w owns chunk W*r+w, two
 // positions per lane (q = c0 + 64*j + lane).  Per chunk:
 //  1. (a) insert every position into the shared table with ds_max_u32 (order-independent ->
 //     deterministic) and into the wave's private table with ds_max_rtn_u32, whose return is
-//     the latest EARLIER position of the chunk with the same 8-bit hash (lanes of one
+//     the latest EARLIER position of the chunk with the same 7-bit hash (lanes of one
 //     instruction are serialised in ascending order on gfx950; verified, see tools/probe_lds);
 //  2. (b) two candidates per position: A = that intra-chunk position, else the shared
 //     table after the round (if it is an earlier position); B = the shared table as of the
@@ -40,8 +40,10 @@ STAMP_MACROS(12)
 
 constexpr uint32_t kFTabBits = 14;
 constexpr uint32_t kFTab = 1u << kFTabBits;   // shared table entries
-constexpr uint32_t kPrivBits = 8;
+constexpr uint32_t kPrivBits = 7;
 constexpr uint32_t kPriv = 1u << kPrivBits;   // private (intra-chunk) table entries per wave
+// A private entry is u64 (pos+1) << 32 | the 4 bytes at pos: ds_max still orders by position,
+// and a candidate taken from it is verified in registers, with no data read.
 constexpr uint32_t kChunk = 128;
 #ifndef SM_FAST_WAVES
 #define SM_FAST_WAVES 16
@@ -51,7 +53,7 @@ constexpr uint32_t kThreads = 64 * kWavesPerBlock;
 constexpr uint32_t kLevels = 5;              // J0..J4: the copy-to-copy walk of a chunk takes <= 31 steps
 constexpr uint32_t kEager = 16;               // bytes compared per candidate before the long-match loop
 #ifndef SM_FAST_NBR
-#define SM_FAST_NBR 4
+#define SM_FAST_NBR 6
 #endif
 constexpr uint32_t kNbr = SM_FAST_NBR;       // earlier chunks of the round probed for candidate C
 
@@ -112,8 +114,8 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = uniform(tid >> 6);
   const uint32_t lane = tid & 63;
-  uint32_t* P = T + kFTab + wave * kPriv;                                     // private table
-  uint32_t* csize = T + kFTab + kWavesPerBlock * kPriv;                       // per-wave chunk sizes
+  uint64_t* P = reinterpret_cast<uint64_t*>(T + kFTab) + wave * kPriv;       // private table
+  uint32_t* csize = T + kFTab + 2 * kWavesPerBlock * kPriv;                   // per-wave chunk sizes
   uint8_t* jt = reinterpret_cast<uint8_t*>(csize + kWavesPerBlock) + wave * kLevels * kChunk;  // parse jump tables
 
   const uint32_t b = blockIdx.x;
@@ -147,7 +149,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   {
     uint4 z = make_uint4(0, 0, 0, 0);
     uint4* t16 = reinterpret_cast<uint4*>(T);
-    for (uint32_t k = tid; k < (kFTab + kWavesPerBlock * kPriv) / 4; k += kThreads) t16[k] = z;
+    for (uint32_t k = tid; k < (kFTab + 2 * kWavesPerBlock * kPriv) / 4; k += kThreads) t16[k] = z;
   }
   uint32_t op = 0;
   if (a.header) {
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     const uint32_t ce = active ? min(c0 + kChunk, n) : c0;
 
     // (a) inserts
-    uint32_t pin[2] = {0, 0};
+    uint64_t pin[2] = {0, 0};
     if (active && !(SM_ABLATE & 4)) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -189,8 +191,8 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         const uint32_t hm = (uint32_t)w[j] * kHashMul;
         if (q + 4 <= n) {
           __hip_atomic_fetch_max(&T[hm >> (32 - kFTabBits)], q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          pin[j] = __hip_atomic_fetch_max(&P[hm >> (32 - kPrivBits)], q + 1, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_WORKGROUP);
+          pin[j] = __hip_atomic_fetch_max(&P[hm >> (32 - kPrivBits)], ((uint64_t)(q + 1) << 32) | (uint32_t)w[j],
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
       }
     }
@@ -203,7 +205,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     uint64_t ts0 = 0, ts1 = 0;
     if (active) {
       // Candidates per position: A = the latest earlier position of the chunk with the same
-      // 8-bit hash (ds_max_rtn above), B = the shared table as of the previous round, C = the
+      // 7-bit hash (ds_max_rtn above), B = the shared table as of the previous round, C = the
       // nearest earlier chunk of this round (waves wave-1..wave-kNbr) whose private table holds
       // a 4-byte match (the positions the round-lagged shared table misses).  The longest
       // match wins (ties: A, B, C).
@@ -213,23 +215,25 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         const uint32_t q = c0 + 64 * j + lane;
         const bool can = q + 4 <= ce;
         const uint64_t wq = w[j];
-        const uint32_t ca = pin[j] > c0 ? pin[j] - 1 : q;
+        const uint32_t pa = (uint32_t)(pin[j] >> 32);
+        const bool oka = pa > c0 && (uint32_t)pin[j] == (uint32_t)wq;  // an earlier chunk position
+        const uint32_t ca = oka ? pa - 1 : q;
         const uint32_t cb = t1[j] != 0 ? t1[j] - 1 : q;
         uint32_t cc = q;
         if (kNbr) {
-          const uint32_t h8 = ((uint32_t)wq * kHashMul) >> (32 - kPrivBits);
-          uint32_t v[kNbr ? kNbr : 1];
+          const uint32_t hp = ((uint32_t)wq * kHashMul) >> (32 - kPrivBits);
+          uint64_t v[kNbr ? kNbr : 1];
 #pragma unroll
-          for (uint32_t m = 1; m <= kNbr; ++m) v[m - 1] = m <= wave ? P[h8 - m * kPriv] : 0u;
+          for (uint32_t m = 1; m <= kNbr; ++m) v[m - 1] = m <= wave ? P[hp - m * kPriv] : 0ull;
 #pragma unroll
           for (int m = (int)kNbr; m >= 1; --m)
-            cc = (v[m - 1] != 0 && lds_ld32(data, v[m - 1] - 1) == (uint32_t)wq) ? v[m - 1] - 1 : cc;
+            cc = ((v[m - 1] >> 32) != 0 && (uint32_t)v[m - 1] == (uint32_t)wq) ? (uint32_t)(v[m - 1] >> 32) - 1 : cc;
         }
         // verify 4 bytes, then grow to 8 and 16; every read is masked to the lanes still
         // matching (an LDS access costs by its active lanes)
         const uint32_t cand[3] = {ca, cb, cc};
         uint32_t len[3];
-        len[0] = (can && ca < q && lds_ld32(data, ca) == (uint32_t)wq) ? 4u : 0u;
+        len[0] = (can && oka) ? 4u : 0u;                                   // verified by its entry
         len[1] = (can && cb < q && cb != ca && lds_ld32(data, cb) == (uint32_t)wq) ? 4u : 0u;
         len[2] = (can && cc < q && cc != ca && cc != cb) ? 4u : 0u;  // verified by the probe
 #pragma unroll
@@ -480,7 +484,7 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 #endif
 
 constexpr size_t kFastLds =
-    kBlockSize + 4 * (kFTab + kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * kLevels * kChunk;
+    kBlockSize + 4 * (kFTab + 2 * kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * kLevels * kChunk;
 static_assert(kFastLds <= 160 * 1024, "fast compressor LDS exceeds a CU");
 
 hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s) {

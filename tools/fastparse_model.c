@@ -20,7 +20,7 @@ static uint32_t copy_bytes(uint32_t off, uint32_t len) {
 
 // policy: 0 = first-chance only (prior rounds), 1 = second chance else first, 2 = best of both,
 //         3 = exact latest-earlier (ideal table)
-static int g_nbr = 0, g_first = 0, g_skip = 0, g_nonempty = 0;  // probe the private tables of g_nbr previous chunks
+static int g_nbr = 0, g_first = 0, g_skip = 0, g_nonempty = 0, g_pbits = 8, g_intrap = 0;  // probe the private tables of g_nbr previous chunks
 
 static uint64_t model_block(const uint8_t* d, uint32_t n, uint32_t chunk, uint32_t waves, uint32_t tab,
                             int policy, int exact_intrachunk) {
@@ -47,7 +47,7 @@ static uint64_t model_block(const uint8_t* d, uint32_t n, uint32_t chunk, uint32
     for (uint32_t k = r * waves; k < (r + 1) * waves && k < nch; ++k) {
       uint32_t c0 = k * chunk, ce = c0 + chunk < n ? c0 + chunk : n;
       memset(P[k - r * waves], 0, sizeof(P[0]));
-      for (uint32_t q = c0; q + 4 <= n && q < ce; ++q) P[k - r * waves][(ld32(d + q) * 0x1e35a7bdu) >> 24] = q + 1;
+      for (uint32_t q = c0; q + 4 <= n && q < ce; ++q) P[k - r * waves][(ld32(d + q) * 0x1e35a7bdu) >> (32 - g_pbits)] = q + 1;
     }
     // second-chance table = max after round (T now)
     for (uint32_t k = r * waves; k < (r + 1) * waves && k < nch; ++k) {
@@ -64,13 +64,18 @@ static uint64_t model_block(const uint8_t* d, uint32_t n, uint32_t chunk, uint32
           else {
             if (policy >= 1 && sc && sc - 1 < p) cands[nc++] = sc;
             if (policy == 0 || policy == 2 || nc == 0) cands[nc++] = cand1[p];
-            if (exact_intrachunk && exact && exact - 1 >= c0) cands[nc++] = exact;
+            if (g_intrap) {  // the kernel's A: latest earlier chunk position with the same private hash
+              uint32_t best_q = 0, hp = (ld32(d + p) * 0x1e35a7bdu) >> (32 - g_pbits);
+              for (uint32_t q = c0; q < p; ++q)
+                if (q + 4 <= n && ((ld32(d + q) * 0x1e35a7bdu) >> (32 - g_pbits)) == hp) best_q = q + 1;
+              if (best_q) cands[nc++] = best_q;
+            } else if (exact_intrachunk && exact && exact - 1 >= c0) cands[nc++] = exact;
           }
           uint32_t nb[64]; int nn = 0, have = 0;
           for (int i = 0; i < nc; ++i)
             if (cands[i] && cands[i] - 1 < p && ld32(d + cands[i] - 1) == ld32(d + p)) have = 1;
           for (int m = 1; m <= g_nbr && !(g_skip && have) && (int)(k - r * waves) - m >= 0; ++m) {
-            uint32_t v = P[k - r * waves - m][(ld32(d + p) * 0x1e35a7bdu) >> 24];
+            uint32_t v = P[k - r * waves - m][(ld32(d + p) * 0x1e35a7bdu) >> (32 - g_pbits)];
             if (g_nonempty) {  // take the nearest non-empty entry, verified or not
               if (!v) continue;
               nb[nn++] = v;
@@ -114,6 +119,8 @@ int main(int argc, char** argv) {
   if (getenv("FIRST")) g_first = 1;
   if (getenv("SKIP")) g_skip = 1;                   // probe only positions without a verified A/B
   if (getenv("NONEMPTY")) g_nonempty = 1;           // nearest non-empty neighbour entry only
+  if (getenv("PBITS")) g_pbits = atoi(getenv("PBITS"));  // private (per-chunk) table hash bits
+  if (getenv("INTRAP")) g_intrap = 1;               // intra-chunk candidate from the private table
   struct { uint32_t chunk, waves, tab; int pol, intra; } cfg[] = {
       {256, 4, 16384, 2, 1}, {256, 8, 16384, 2, 1}, {128, 8, 16384, 2, 1}, {256, 8, 16384, 1, 1},
       {256, 4, 12288, 2, 1}, {256, 8, 12288, 2, 1}, {256, 4, 8192, 2, 1}, {256, 8, 8192, 2, 1},
