@@ -64,6 +64,12 @@ sm_status sm_uncompressed_length(const char* compressed, size_t compressed_lengt
 sm_status sm_parse32(const uint8_t* buf, size_t len, size_t off, uint32_t* value, size_t* next);
 /* replaces encode32!, src/varint.jl:46-69.  Writes 1..5 bytes, returns the count. */
 size_t sm_encode32(uint8_t* buf, uint32_t value);
+/* replaces find_match_length, src/internal.jl:343-387 (host; the reference's tests call it,
+ * test/runtests.jl:168-267).  0-based i1 < i2, limit INCLUSIVE: the length of the common run
+ * of buf[i1..] and buf[i2..] with i2 + n - 1 <= limit.  SM_ERR_ARGUMENT where the reference
+ * would read past buf (its @test_broken case). */
+sm_status sm_find_match_length(const uint8_t* buf, size_t len, size_t i1, size_t i2, size_t limit,
+                               size_t* matched);
 
 /* ---- device context -------------------------------------------------------------- */
 sm_ctx* sm_ctx_create(int device);

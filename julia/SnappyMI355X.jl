@@ -46,4 +46,26 @@ function uncompress(input::Vector{UInt8})           # src/Snappy.jl:46
     st == 0 || error(status_message(st))            # the reference's exact message text
     return output
 end
+
+# helpers the reference's own tests call (test/runtests.jl:96-173), 1-based like the reference
+function parse32(buf::Vector{UInt8}, offset::Integer)                 # src/varint.jl:12
+    v = Ref{UInt32}(0); nx = Ref{Csize_t}(0)
+    st = ccall((:sm_parse32, LIB), Cint, (Ptr{UInt8}, Csize_t, Csize_t, Ref{UInt32}, Ref{Csize_t}),
+               buf, length(buf), offset - 1, v, nx)
+    st == 0 || error(status_message(st))
+    return (v[], Int(nx[]) + 1)
+end
+function encode32!(buf::Vector{UInt8}, offset::Integer, value::UInt32)  # src/varint.jl:46
+    tmp = Vector{UInt8}(undef, 5)
+    n = ccall((:sm_encode32, LIB), Csize_t, (Ptr{UInt8}, UInt32), tmp, value)
+    buf[offset:offset+n-1] = tmp[1:n]
+    return offset + n
+end
+function find_match_length(a::Vector{UInt8}, i1::Integer, i2::Integer, limit::Integer)  # internal.jl:343
+    m = Ref{Csize_t}(0)
+    st = ccall((:sm_find_match_length, LIB), Cint, (Ptr{UInt8}, Csize_t, Csize_t, Csize_t, Csize_t, Ref{Csize_t}),
+               a, length(a), i1 - 1, i2 - 1, limit - 1, m)
+    st == 0 || throw(BoundsError(a, limit))   # the reference reads past `a` here (@test_broken)
+    return Int(m[])
+end
 end

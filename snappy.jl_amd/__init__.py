@@ -40,6 +40,7 @@ ABI_SYMBOLS = (
     "sm_encode32", "sm_ctx_create", "sm_ctx_destroy", "sm_ctx_stream", "sm_compress", "sm_uncompress",
     "sm_compress_batch_device", "sm_uncompress_batch_device", "sm_compress_batch",
     "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device", "sm_ctx_last_path",
+    "sm_find_match_length",
 )
 
 
@@ -95,6 +96,8 @@ def lib():
         L.sm_compress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
         L.sm_uncompress_batch.restype = i32
         L.sm_uncompress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+        L.sm_find_match_length.restype = i32
+        L.sm_find_match_length.argtypes = [vp, sz, sz, sz, sz, ctypes.POINTER(sz)]
         L.sm_ctx_last_path.restype = ctypes.c_int
         L.sm_ctx_last_path.argtypes = [vp]
         L.sm_version.restype = ctypes.c_char_p
@@ -176,6 +179,18 @@ def compress(data, mode="reference", device=0):
     if st:
         raise SnappyError(st)
     return out[: ol.value].tobytes()
+
+
+def find_match_length(buf, i1, i2, limit):
+    """internal.jl:343-387 (0-based i1 < i2, inclusive limit); SnappyError where the
+    reference would read past buf."""
+    src = _bytes(buf)
+    res = ctypes.c_size_t(0)
+    st = lib().sm_find_match_length(src.ctypes.data if src.size else None, src.size, i1, i2, limit,
+                                    ctypes.byref(res))
+    if st:
+        raise SnappyError(st)
+    return res.value
 
 
 def last_uncompress_path(device=0):

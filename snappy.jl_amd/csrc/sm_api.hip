@@ -218,6 +218,37 @@ size_t sm_encode32(uint8_t* buf, uint32_t v) {
   return i;
 }
 
+sm_status sm_find_match_length(const uint8_t* buf, size_t len, size_t i1, size_t i2, size_t limit,
+                               size_t* matched) {
+  if (!matched || (len && !buf)) return SM_ERR_ARGUMENT;
+  // 8 bytes at a time while i2 + 7 <= limit, then bytes (internal.jl:356-386); every read
+  // the reference makes must lie inside buf
+  auto ld64 = [&](size_t i, uint64_t* v) {
+    if (i + 8 > len) return false;
+    memcpy(v, buf + i, 8);
+    return true;
+  };
+  size_t m = 0;
+  while (i2 + 7 <= limit) {
+    uint64_t a, b;
+    if (!ld64(i1 + m, &a) || !ld64(i2, &b)) return SM_ERR_ARGUMENT;
+    if (a != b) {
+      *matched = m + (__builtin_ctzll(a ^ b) >> 3);
+      return SM_OK;
+    }
+    i2 += 8;
+    m += 8;
+  }
+  while (i2 <= limit) {
+    if (i2 >= len || i1 + m >= len) return SM_ERR_ARGUMENT;
+    if (buf[i1 + m] != buf[i2]) break;
+    ++i2;
+    ++m;
+  }
+  *matched = m;
+  return SM_OK;
+}
+
 sm_status sm_uncompressed_length(const char* compressed, size_t n, size_t* result) {
   uint32_t v = 0;
   sm_status st = sm_parse32((const uint8_t*)compressed, n, 0, &v, nullptr);

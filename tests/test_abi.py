@@ -87,3 +87,15 @@ def test_ctx_create_without_gpu_returns_null(sm):
     assert not sm.lib().sm_ctx_create(0)
     with pytest.raises(sm.SnappyError):
         sm.compress(b"abc")
+
+
+@pytest.mark.parametrize("a,b,limit,expected", __import__("test_oracle").FML_KATS)
+def test_find_match_length_kat_abi(sm, a, b, limit, expected):
+    """The C ABI's find_match_length (host) on the reference's known-answer tests
+    (test/runtests.jl:176-267); the @test_broken case reads past the array -> an error."""
+    c = (a + b).encode("latin-1")
+    if expected is None:
+        with pytest.raises(sm.SnappyError):
+            sm.find_match_length(c, 0, len(a), len(a) + limit - 1)
+    else:
+        assert sm.find_match_length(c, 0, len(a), len(a) + limit - 1) == expected
