@@ -190,6 +190,50 @@ __device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t from
   if (lane < to - from) out[from + lane] = win[(from + lane) & (kWin - 1)];
 }
 
+// Tag walk over a 256-byte window by pointer doubling (VALU + LDS, no serial loop).
+// cw = the 8 stream bytes at window position 4*lane; rlim (<= 256) = the parse limit relative
+// to the window (window end or N-1, internal.jl:416).  Every lane computes the speculative
+// sizes of its 4 positions (packed u8 in `sizes`, 255 = a literal too long for a batch).
+// J0[p] = p + size(p); a long literal or a position at/after rlim is a stop node (J0[p] = p).
+// J_k = J_{k-1} o J_{k-1}, k < kWalkLevels: 64 tags = chain elements 0..63 from position 0.
+// Lane t then holds tag t directly -- J_k applied for every set bit k of t -- with its window
+// position cpos and size csz; stop nodes are fixed points, so the tags are a prefix of
+// lanes.  Returns their count.
+__device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt, uint32_t lane, uint32_t& cpos,
+                                       uint32_t& csz, uint32_t& sizes) {
+  sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
+  uint32_t J[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint32_t p = 4 * lane + j;
+    const uint32_t sz = (sizes >> (8 * j)) & 0xff;
+    J[j] = (sz == 255 || p >= rlim) ? p : p + sz;
+  }
+  *reinterpret_cast<uint2*>(jt + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+#pragma unroll
+  for (int k = 1; k < kWalkLevels; ++k) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint16_t* prev = jt + (k - 1) * 256;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) J[j] = J[j] < 256 ? prev[J[j]] : J[j];
+    *reinterpret_cast<uint2*>(jt + k * 256 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the u16 reads below follow the uint2 stores
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < kWalkLevels; ++k) {
+    const uint32_t t = c < 256 ? jt[k * 256 + c] : c;
+    c = ((lane >> k) & 1u) ? t : c;
+  }
+  // (the shuffle runs with every lane active: a ds_bpermute from an inactive lane reads 0)
+  const uint32_t szw = __shfl(sizes, (c >> 2) & 63u, 64);
+  const uint32_t sz = c < 256 ? (szw >> (8 * (c & 3))) & 0xffu : 0u;
+  cpos = c;
+  csz = sz;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the next walk's stores follow these reads
+  return (uint32_t)__builtin_popcountll(ballot(c < rlim && sz != 255));
+}
+
 // Decodes the tags that start in [ip, ip_end) -- ip_end = N for a whole stream, whose loop
 // stops at N-1 (internal.jl:416) -- into out[op0, ...).  Copy sources below frag_lo are
 // refused with kErrCross: a fragment of a block-structured stream must not read output that
@@ -225,51 +269,11 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
     }
     STAMP(0)
-    // speculative tag sizes for the window [ip, ip+256) (inside the ring: ip < wb+256; a
-    // batch's literals end before ip+256+200 < wb+768)
-    const uint64_t cw = ring_get8(ring, ip + 4 * lane);
-    const uint32_t sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
-
-    // Parallel tag walk by pointer doubling over the 256 window positions (VALU + LDS, no
-    // serial SALU loop).  J0[p] = p + size(p); a position whose tag is a long literal, or that
-    // lies at/after the parse limit (window end or N-1, internal.jl:416), is a stop node
-    // (J0[p] = p, self-loop).  J_k = J_{k-1} o J_{k-1}, k < kWalkLevels (a batch takes at most
-    // 64 tags, chain elements 0..63 steps from the window's first position, ip).
+    // the window [ip, ip+256) (inside the ring: ip < wb+256; a batch's literals end before
+    // ip+256+200 < wb+768)
     const uint32_t wlim = (int64_t)(ip + 256) < Nm1 ? ip + 256 : (uint32_t)Nm1;
-    const uint32_t rlim = wlim - ip;
-    uint32_t J[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t p = 4 * lane + j;
-      const uint32_t sz = (sizes >> (8 * j)) & 0xff;
-      J[j] = (sz == 255 || p >= rlim) ? p : p + sz;
-    }
-    uint16_t* jt0 = jt;
-    *reinterpret_cast<uint2*>(jt0 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
-#pragma unroll
-    for (int k = 1; k < kWalkLevels; ++k) {
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      const uint16_t* prev = jt + (k - 1) * 256;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) J[j] = J[j] < 256 ? prev[J[j]] : J[j];
-      *reinterpret_cast<uint2*>(jt + k * 256 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the u16 reads below follow the uint2 stores
-    // Tag t of the batch sits in lane t: apply J_k for every set bit k of t to position 0
-    // (chain element t).  Stop nodes are fixed points, so the lanes past the batch's last tag
-    // all land on the first stop (or beyond the window) -- the tags are a prefix of lanes.
-    uint32_t cpos = 0;
-#pragma unroll
-    for (int k = 0; k < kWalkLevels; ++k) {
-      const uint32_t t = cpos < 256 ? jt[k * 256 + cpos] : cpos;
-      cpos = ((lane >> k) & 1u) ? t : cpos;
-    }
-    // (the shuffle runs with every lane active: a ds_bpermute from an inactive lane reads 0)
-    const uint32_t szw = __shfl(sizes, (cpos >> 2) & 63u, 64);
-    const uint32_t csz = cpos < 256 ? (szw >> (8 * (cpos & 3))) & 0xffu : 0u;
-    const bool ctag = cpos < rlim && csz != 255;  // rlim <= 256
-    const uint64_t tm = ballot(ctag);
-    const uint32_t ntok = (uint32_t)__builtin_popcountll(tm);
+    uint32_t cpos, csz, sizes;
+    const uint32_t ntok = walk_window(ring_get8(ring, ip + 4 * lane), wlim - ip, jt, lane, cpos, csz, sizes);
     uint32_t tpos = 0, ipw = ip, tnext = 0;
     bool big = false;
     if (ntok) {
@@ -569,14 +573,14 @@ __global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
 // independently, so in their streams every output multiple of 65536 is a tag start and no copy
 // reaches into an earlier block.  Finding those tags needs the tag boundaries, which the format
 // does not index:
-//  1. k_stream_index, one wave per 4 KiB chunk of the compressed body: lane 0 walks the tags
-//     speculatively from the chunk's first byte, recording each visited position and the output
-//     before it; lanes l = 1..63 walk from byte l until they meet lane 0's path (tag walks
+//  1. k_stream_index, one wave per 4 KiB chunk of the compressed body: the wave walks the tags
+//     speculatively from the chunk's first byte (walk_window, 256 bytes per step: "lane 0's
+//     path"), recording each visited position and the output before it; lanes l = 1..63 walk from byte l until they meet lane 0's path (tag walks
 //     resynchronise within a few tags on compressible data) or leave the chunk.  Each chunk then
 //     knows, for entry offsets 0..63, where the walk leaves it and how much output it makes.
 //  2. The host chains the true path (sm_api.hip) and locates each fragment's chunk.
-//  3. k_decompress_frags, one wave per fragment: walk from the chunk entry to the tag at output
-//     F, then the batch engine with frag_lo = F and the output limit F + 65536.
+//  3. k_decompress_frags, one wave per fragment: walk (window-parallel) from the chunk entry to
+//     the tag at output F, then the batch engine with frag_lo = F and the output limit F + 65536.
 // Anything unexpected (kErrCross, an error, a length mismatch) sends the caller to the in-order
 // decode, which reproduces the reference's accept/reject exactly.
 
@@ -605,27 +609,57 @@ __device__ inline void stage_bytes(uint8_t* buf, const uint8_t* __restrict__ in,
   for (uint32_t k = lane; k < len; k += kWave) buf[k] = s + k < N ? in[s + k] : 0;
 }
 
+// Tags of the staged window at chunk byte rel0 (walk_window over buf, rlim <= 256): lane t <
+// ntok gets tag t's chunk position, its output bytes and the exclusive scan of them.  ntok == 0
+// means a long literal (or nothing parseable) at rel0: the caller takes one scalar step.
+__device__ inline uint32_t window_tags(const uint8_t* buf, uint32_t rel0, uint32_t rlim, uint16_t* jt, uint32_t lane,
+                                       uint32_t& rel, uint32_t& next, uint32_t& outb, uint32_t& excl) {
+  uint32_t cpos, csz, sizes;
+  const uint32_t ntok = walk_window(lds_ld64(buf, rel0 + 4 * lane), rlim, jt, lane, cpos, csz, sizes);
+  const bool mine = lane < ntok;
+  const uint32_t c = buf[rel0 + (mine ? cpos : 0u)];
+  const uint32_t e = char_entry(c);
+  outb = !mine ? 0u : (c & 3) ? (e & 0xff) : csz - 1 - (e >> 11);  // a batch literal: csz = 1 + taglen + len
+  excl = scan_dpp(outb) - outb;
+  rel = rel0 + cpos;
+  next = rel + csz;
+  return ntok;
+}
+
 __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
                                                      uint32_t* rec_exit, uint32_t* rec_out) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kIdxChunk + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kIdxChunk + kIdxPad];
+  __shared__ __attribute__((aligned(16))) uint16_t jt[kWalkLevels * 256];
   __shared__ uint32_t bm[kIdxChunk / 32];  // positions on lane 0's path
   __shared__ uint32_t cum[kIdxChunk];      // output before each such position
   const uint32_t c = blockIdx.x, lane = lane_id();
   const uint32_t s = ip0 + c * kIdxChunk;
-  stage_bytes(buf, in, N, s, kIdxChunk + 16, lane);
+  stage_bytes(buf, in, N, s, kIdxChunk + kIdxPad, lane);
   for (uint32_t k = lane; k < kIdxChunk / 32; k += kWave) bm[k] = 0;
   __syncthreads();
   const uint64_t lim = min((uint64_t)s + kIdxChunk, (uint64_t)N - 1);  // tags start below N-1 (:416)
+  // lane 0's path: the tag walk from the chunk's first byte, a 256-byte window at a time
   uint64_t p = s, acc = 0, size, outb;
-  while (p < lim) {  // lane 0's path, wave-uniform
-    const uint32_t rel = (uint32_t)(p - s);
-    if (lane == 0) {
-      bm[rel >> 5] |= 1u << (rel & 31);
-      cum[rel] = (uint32_t)acc;
+  while (p < lim) {
+    const uint32_t rel0 = (uint32_t)(p - s);
+    uint32_t rel, next, ob, excl;
+    const uint32_t ntok = window_tags(buf, rel0, (uint32_t)min(lim - p, (uint64_t)256), jt, lane, rel, next, ob, excl);
+    if (ntok == 0) {  // long literal
+      if (lane == 0) {
+        bm[rel0 >> 5] |= 1u << (rel0 & 31);
+        cum[rel0] = (uint32_t)acc;
+      }
+      tag_at(buf, rel0, size, outb);
+      acc += outb;
+      p += size;
+      continue;
     }
-    tag_at(buf, rel, size, outb);
-    acc += outb;
-    p += size;
+    if (lane < ntok) {
+      atomicOr(&bm[rel >> 5], 1u << (rel & 31));
+      cum[rel] = (uint32_t)acc + excl;
+    }
+    acc += readlane(excl + ob, ntok - 1);
+    p = s + readlane(next, ntok - 1);
   }
   __syncthreads();
   const uint64_t exit0 = p;
@@ -662,22 +696,38 @@ __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __res
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
   __shared__ __attribute__((aligned(16))) uint16_t sjt[kWalkLevels * 256];
   __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];
-  __shared__ __attribute__((aligned(16))) uint8_t sbuf[kIdxChunk + 32];
+  __shared__ __attribute__((aligned(16))) uint8_t sbuf[kIdxChunk + kIdxPad];
   const uint32_t f = blockIdx.x, lane = lane_id();
   const StreamFrag fr = frags[f];
-  // walk from the chunk entry to the tag that starts at output F (inside that chunk)
-  stage_bytes(sbuf, in, N, fr.y, kIdxChunk + 32, lane);
+  // walk from the chunk entry to the tag that starts at output F (inside that chunk), a
+  // 256-byte window at a time: the first tag whose preceding output reaches F
+  stage_bytes(sbuf, in, N, fr.y, kIdxChunk + kIdxPad, lane);
   __syncthreads();
   uint64_t p = fr.y, o = fr.O, tsz, outb;
   int32_t st = kOk;
   while (o < fr.F) {
-    if (p - fr.y >= kIdxChunk + 16) {
+    const uint32_t rel0 = (uint32_t)(p - fr.y);
+    if (rel0 >= kIdxChunk + 16) {
       st = kErrCross;
       break;
     }
-    tag_at(sbuf, (uint32_t)(p - fr.y), tsz, outb);
-    o += outb;
-    p += tsz;
+    uint32_t rel, next, ob, excl;
+    const uint32_t ntok = window_tags(sbuf, rel0, min(kIdxChunk + 16 - rel0, 256u), sjt, lane, rel, next, ob, excl);
+    if (ntok == 0) {  // long literal
+      tag_at(sbuf, rel0, tsz, outb);
+      o += outb;
+      p += tsz;
+      continue;
+    }
+    const uint64_t hit = ballot(lane < ntok && o + excl >= fr.F);
+    if (hit) {
+      const uint32_t t = ctz64(hit);
+      o += readlane(excl, t);
+      p = fr.y + readlane(rel, t);
+      break;
+    }
+    o += readlane(excl + ob, ntok - 1);
+    p = fr.y + readlane(next, ntok - 1);
   }
   if (st == kOk && o != fr.F) st = kErrCross;  // no tag starts at F: not block-structured
   if (st == kOk) {

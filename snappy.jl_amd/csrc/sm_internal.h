@@ -41,6 +41,7 @@ hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 // compressed body, then one wave per 64 KiB output fragment (see sm_decompress.hip).
 constexpr uint32_t kIdxChunk = 4096;  // compressed bytes per index chunk
 constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
+constexpr uint32_t kIdxPad = 288;     // staged bytes past a chunk: +16 entry slack, a 256-byte walk window + 16
 struct StreamFrag {
   uint32_t y;    // a true tag start at or before the fragment's first tag (chunk entry)
   uint32_t O;    // output position of the tag at y
