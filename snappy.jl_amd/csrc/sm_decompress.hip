@@ -36,6 +36,10 @@
 #define SM_ABLATE_D 0
 #endif
 
+#ifndef SM_IDX_NOLANES
+#define SM_IDX_NOLANES 0
+#endif
+
 namespace sm {
 
 #if SM_STAMP
@@ -48,6 +52,7 @@ typedef uint32_t __attribute__((aligned(1))) du32u;
 typedef uint64_t __attribute__((aligned(1))) du64u;
 
 constexpr uint32_t kRing = 1024;
+constexpr uint32_t kMaxBatchLit = 200;  // longer literals stop a window walk (size 255)
 constexpr int kWalkLevels = 6;  // J0..J5: 63 steps = the 64 tags of a batch
 constexpr int kPass = 2;        // 8-byte chunks per execution pass (most tags are <= 16 B)
 
@@ -70,7 +75,7 @@ __device__ inline uint32_t spec_size(uint32_t c, uint32_t trailer) {
   uint32_t len = entry & 0xff;
   uint32_t tr = taglen >= 4 ? trailer : (trailer & ((1u << (8 * taglen)) - 1u));
   uint32_t lit = len + tr;  // u32 wrap, as the reference
-  return lit > 200 ? 255u : 1 + taglen + lit;
+  return lit > kMaxBatchLit ? 255u : 1 + taglen + lit;
 }
 
 __device__ inline uint32_t pack_sizes_slow(uint32_t cur, uint32_t nxt) {
@@ -606,7 +611,31 @@ __device__ inline void tag_at(const uint8_t* buf, uint32_t rel, uint64_t& size, 
 // bytes [s, s+len) of the stream into LDS, zero past N (the reference's zero-padded lookahead)
 __device__ inline void stage_bytes(uint8_t* buf, const uint8_t* __restrict__ in, uint32_t N, uint32_t s, uint32_t len,
                                    uint32_t lane) {
-  for (uint32_t k = lane; k < len; k += kWave) buf[k] = s + k < N ? in[s + k] : 0;
+  // dword k = stream bytes [s+4k, s+4k+4): two aligned global dwords + v_alignbyte, all of a
+  // lane's loads issued before its LDS stores (len % 256 == 0 words per lane is not assumed)
+  constexpr int kU = 6;
+  const uint32_t mis = (uint32_t)((uintptr_t)(in + s) & 3u);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(in + s - mis);
+  const uint32_t nw = (len + 3) / 4;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(buf);
+  for (uint32_t k0 = lane; k0 < nw; k0 += kU * kWave) {
+    uint32_t w[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint32_t k = k0 + u * kWave;
+      const uint64_t b = (uint64_t)s + 4 * k;  // stream offset of word k
+      if (k < nw && s >= mis && b - mis + 8 <= N) {
+        w[u] = __builtin_amdgcn_alignbyte(src[k + 1], src[k], mis);
+      } else {
+        uint32_t v = 0;
+        for (uint32_t j = 0; j < 4; ++j) v |= (b + j < N ? (uint32_t)in[b + j] : 0u) << (8 * j);
+        w[u] = v;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (k0 + u * kWave < nw) dst[k0 + u * kWave] = w[u];
+  }
 }
 
 // Tags of the staged window at chunk byte rel0 (walk_window over buf, rlim <= 256): lane t <
@@ -664,28 +693,81 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
   __syncthreads();
   const uint64_t exit0 = p;
   const uint32_t tot0 = (uint32_t)acc;
-  uint64_t q = (uint64_t)s + lane, ex = exit0;
+  // Lanes 1..63 (entries at chunk bytes 1..63) walk until they meet lane 0's path or leave the
+  // chunk, a 256-byte window at a time, by pointer doubling with lane 0's path as stop nodes:
+  // J0[x] = x + size(x), O0[x] = its output bytes; a path position, a long literal or a
+  // position at/after the limit is a fixed point (O = 0).  Seven doublings give 128 steps --
+  // more tags than 256 bytes hold -- so J7[x] is where the walk from x meets the path, stops or
+  // leaves the window, and O7[x] the output on the way.  Long literals take a scalar step.
+  const uint64_t rl = lim > s ? lim - s : 0;  // chunk-relative parse limit
+  uint64_t x = lane, ex = exit0;
   uint32_t pre = 0, res = tot0;
-  bool done = lane == 0;
-  while (ballot(!done)) {
-    if (!done) {
-      if (q >= lim) {
-        ex = q;
-        res = pre;
-        done = true;
-      } else {
-        const uint32_t rel = (uint32_t)(q - s);
-        if ((bm[rel >> 5] >> (rel & 31)) & 1u) {  // met lane 0's path
-          ex = exit0;
-          res = pre + (tot0 - cum[rel]);
+  bool done = lane == 0 || SM_IDX_NOLANES;  // (SM_IDX_NOLANES: timing variant only)
+  uint16_t* tj = jt;                                   // 2 x 256 u16
+  uint32_t* to = reinterpret_cast<uint32_t*>(jt + 512);  // 2 x 256 u32 (jt holds 3 KiB)
+  while (true) {
+    bool again = true;
+    while (ballot(again)) {  // settle: out of the chunk, on the path, or a long literal
+      again = false;
+      if (!done) {
+        if (x >= rl) {
+          ex = s + x;
+          res = pre;
+          done = true;
+        } else if ((bm[x >> 5] >> (x & 31)) & 1u) {  // met lane 0's path
+          res = pre + (tot0 - cum[x]);
           done = true;
         } else {
-          tag_at(buf, rel, size, outb);
-          pre += (uint32_t)outb;
-          q += size;
+          tag_at(buf, (uint32_t)x, size, outb);
+          if ((buf[x] & 3) == 0 && outb > kMaxBatchLit) {
+            pre += (uint32_t)outb;
+            x += size;
+            again = true;
+          }
         }
       }
     }
+    if (!ballot(!done)) break;
+    uint32_t base = done ? 0xffffffffu : (uint32_t)x;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) base = min(base, (uint32_t)__shfl_xor(base, d, 64));
+    const uint32_t rlim = (uint32_t)min(rl - base, (uint64_t)256);
+    const uint64_t cw = lds_ld64(buf, base + 4 * lane);
+    const uint32_t sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
+    uint32_t J[4], O[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t r = 4 * lane + j, a = base + r, sz = (sizes >> (8 * j)) & 0xff, cb = (uint32_t)(cw >> (8 * j)) & 0xff;
+      const uint32_t e = char_entry(cb);
+      const bool stop = r >= rlim || ((bm[a >> 5] >> (a & 31)) & 1u) || sz == 255;  // (bm read below rlim only)
+      J[j] = stop ? r : r + sz;
+      O[j] = stop ? 0u : (cb & 3) ? (e & 0xff) : sz - 1 - (e >> 11);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // k = 7: the final tables for the lanes' read
+      uint16_t* bj = tj + (k & 1) * 256;
+      uint32_t* bo = to + (k & 1) * 256;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        bj[4 * lane + j] = (uint16_t)J[j];
+        bo[4 * lane + j] = O[j];
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (k == 7) break;
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (J[j] < 256) {
+          O[j] += bo[J[j]];
+          J[j] = bj[J[j]];
+        }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    if (!done && x < base + 256) {
+      const uint32_t r = (uint32_t)x - base;
+      pre += to[256 + r];
+      x = base + tj[256 + r];
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the next window's stores follow these reads
   }
   rec_exit[c * kIdxEntries + lane] = (uint32_t)min(ex, (uint64_t)0xffffffffu);
   rec_out[c * kIdxEntries + lane] = res;
