@@ -235,6 +235,11 @@ def main():
 
     extras = {}
     if args.extras:
+        # validation (the decoder's walk + checks, no output) of the fast streams
+        vst = torch.full_like(batch.status, -1)
+        t_v = time_kernel(lambda: sm.validate_batch_device(batch.d_comp, batch.comp_off, batch.comp_len, vst), 3)
+        ok = ok and int(vst.abs().sum()) == 0
+        extras["validate_GBps"] = round(in_bytes / (t_v * 1e-3) / 1e9, 3)
         t_ref = time_kernel(lambda: batch.compress(sm, "reference"), 1)
         extras["reference_mode_compress_GBps"] = round(in_bytes / (t_ref * 1e-3) / 1e9, 3)
         # config 3 with the exact (Snappy.jl byte-identical) streams as input

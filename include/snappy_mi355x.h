@@ -118,12 +118,28 @@ sm_status sm_uncompress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uin
                                      const uint64_t* d_out_off, const uint32_t* d_out_cap,
                                      uint32_t* d_out_len, int32_t* d_status, void* stream);
 
+/* Block b: d_status[b] = exactly the status uncompress(block) would return
+ * (src/Snappy.jl:46-52 with the checks of src/internal.jl:411-527) given enough output room,
+ * found by the decoder's tag walk and checks alone -- no output is written.  Batched
+ * snappy_validate_compressed_buffer (snappy-c.h), SURVEY §8(f) row 4. */
+sm_status sm_validate_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                   const uint32_t* d_in_len, uint32_t nblk, int32_t* d_status, void* stream);
+/* Block b: d_len[b] = its declared uncompressed length (the varint header) and d_status[b] =
+ * SM_OK, or SM_ERR_VARINT with d_len[b] = 0.  Batched length_uncompressed, src/Snappy.jl:90-92. */
+sm_status sm_uncompressed_length_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                              const uint32_t* d_in_len, uint32_t nblk, uint32_t* d_len,
+                                              int32_t* d_status, void* stream);
+
 /* ---- batched, host memory (H2D + kernel + D2H, synchronous) ------------------------ */
 sm_status sm_compress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                             uint32_t nblk, uint8_t* out, const uint64_t* out_off, uint32_t* out_len, int mode);
 sm_status sm_uncompress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                               uint32_t nblk, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                               uint32_t* out_len, int32_t* status);
+
+/* snappy_validate_compressed_buffer (snappy-c.h) for one host buffer, on the device: the status
+ * sm_uncompress would return with enough output room, without decoding into memory. */
+sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, size_t compressed_length);
 
 /* library build identification ("snappy_mi355x gfx950 <git-describe>") */
 const char* sm_version(void);

@@ -40,7 +40,8 @@ ABI_SYMBOLS = (
     "sm_encode32", "sm_ctx_create", "sm_ctx_destroy", "sm_ctx_stream", "sm_compress", "sm_uncompress",
     "sm_compress_batch_device", "sm_uncompress_batch_device", "sm_compress_batch",
     "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device", "sm_ctx_last_path",
-    "sm_find_match_length",
+    "sm_find_match_length", "sm_validate_batch_device", "sm_uncompressed_length_batch_device",
+    "sm_validate_compressed_buffer",
 )
 
 
@@ -104,6 +105,12 @@ def lib():
         L.sm_version.argtypes = []
         L.sm_compress_fragments_device.restype = i32
         L.sm_compress_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp]
+        L.sm_validate_batch_device.restype = i32
+        L.sm_validate_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp]
+        L.sm_uncompressed_length_batch_device.restype = i32
+        L.sm_uncompressed_length_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
+        L.sm_validate_compressed_buffer.restype = i32
+        L.sm_validate_compressed_buffer.argtypes = [vp, vp, sz]
         _lib = L
     return _lib
 
@@ -285,6 +292,13 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _stream(stream, dev):
+    import torch
+    if stream is None:
+        return torch.cuda.current_stream(dev).cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else stream
+
+
 def compress_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, mode="fast", stream=None,
                           device=None):
     """All arguments are torch CUDA tensors (uint8 / int64 / int32).  Asynchronous on `stream`
@@ -331,6 +345,33 @@ def uncompress_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_ca
                                           _ptr(d_out_len), _ptr(d_status), ctypes.c_void_p(stream))
     if st:
         raise SnappyError(st)
+
+
+def validate_batch_device(d_in, d_in_off, d_in_len, d_status, stream=None, device=None):
+    """d_status[b] = the status uncompress(block b) would return (no output written):
+    batched snappy_validate_compressed_buffer."""
+    dev = d_in.device.index if device is None else device
+    st = lib().sm_validate_batch_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len), d_in_len.numel(),
+                                        _ptr(d_status), ctypes.c_void_p(_stream(stream, dev)))
+    if st:
+        raise SnappyError(st)
+
+
+def uncompressed_length_batch_device(d_in, d_in_off, d_in_len, d_len, d_status, stream=None, device=None):
+    """Batched length_uncompressed (Snappy.jl:90-92): the varint header of every block."""
+    dev = d_in.device.index if device is None else device
+    st = lib().sm_uncompressed_length_batch_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len),
+                                                   d_in_len.numel(), _ptr(d_len), _ptr(d_status),
+                                                   ctypes.c_void_p(_stream(stream, dev)))
+    if st:
+        raise SnappyError(st)
+
+
+def validate(data, device=0):
+    """snappy_validate_compressed_buffer on the GPU: SM_OK (0) or the status uncompress(data)
+    would raise with."""
+    src = _bytes(data)
+    return int(lib().sm_validate_compressed_buffer(context(device), src.ctypes.data if src.size else None, src.size))
 
 
 def version():

@@ -413,6 +413,50 @@ sm_status sm_uncompress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in
   return SM_OK;
 }
 
+sm_status sm_validate_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                   const uint32_t* d_in_len, uint32_t nblk, int32_t* d_status, void* stream) {
+  if (!ctx) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_status) return SM_ERR_ARGUMENT;
+  DeviceGuard g(ctx->device);
+  SM_CHECK(sm::launch_validate(d_in, d_in_off, d_in_len, nblk, d_status, (hipStream_t)stream));
+  return SM_OK;
+}
+
+sm_status sm_uncompressed_length_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                              const uint32_t* d_in_len, uint32_t nblk, uint32_t* d_len,
+                                              int32_t* d_status, void* stream) {
+  if (!ctx) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_len || !d_status) return SM_ERR_ARGUMENT;
+  DeviceGuard g(ctx->device);
+  SM_CHECK(sm::launch_uncompressed_length(d_in, d_in_off, d_in_len, nblk, d_len, d_status, (hipStream_t)stream));
+  return SM_OK;
+}
+
+sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, size_t n) {
+  if (!ctx || (n && !compressed)) return SM_ERR_ARGUMENT;
+  if (n > 0xffffffffull) return SM_ERR_ARGUMENT;
+  DeviceGuard g(ctx->device);
+  hipStream_t s = ctx->stream;
+  SM_CHECK(ctx->in.ensure(n + 16));
+  SM_CHECK(ctx->meta.ensure(64));
+  uint8_t* m = (uint8_t*)ctx->meta.p;
+  uint64_t* d_off = (uint64_t*)m;
+  uint32_t* d_len = (uint32_t*)(m + 8);
+  int32_t* d_status = (int32_t*)(m + 12);
+  const uint64_t zero = 0;
+  const uint32_t len32 = (uint32_t)n;
+  int32_t st = SM_ERR_DEVICE;
+  if (n) SM_CHECK(hipMemcpyAsync(ctx->in.p, compressed, n, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_off, &zero, 8, hipMemcpyHostToDevice, s));
+  SM_CHECK(hipMemcpyAsync(d_len, &len32, 4, hipMemcpyHostToDevice, s));
+  SM_CHECK(sm::launch_validate((const uint8_t*)ctx->in.p, d_off, d_len, 1, d_status, s));
+  SM_CHECK(hipMemcpyAsync(&st, d_status, 4, hipMemcpyDeviceToHost, s));
+  SM_CHECK(hipStreamSynchronize(s));
+  return st;
+}
+
 // src/Snappy.jl:20-36 on the device: every 64 KiB fragment is one wave; fragments use the
 // table size of the WHOLE input (Q2) and no per-fragment header; a gather kernel then
 // concatenates them behind the varint header.

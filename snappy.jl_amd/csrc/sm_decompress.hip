@@ -528,24 +528,16 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   return kOk;
 }
 
-__global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t sjt[kWalkLevels * 256];  // tag-walk jump tables
-  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];                // output window
-  const uint32_t b = blockIdx.x;
-  const uint32_t lane = lane_id();
-  const uint8_t* in = a.in + a.in_off[b];
-  const uint32_t N = a.in_len[b];
-  uint8_t* dst = a.out + a.out_off[b];
-  const uint32_t cap = a.out_cap[b];
-
-  // varint32 header (varint.jl:12-37)
-  uint32_t hb = (lane < 5 && lane < N) ? in[lane] : 0;
+// varint32 stream header (varint.jl:12-37): size and the first tag's position; kErrVarint on
+// more than 5 bytes, a 5th byte >= 0x10 or a truncated header
+__device__ inline int32_t parse_header(const uint8_t* in, uint32_t N, uint32_t lane, uint32_t& size, uint32_t& ip) {
+  const uint32_t hb = (lane < 5 && lane < N) ? in[lane] : 0;
   int32_t st = kErrVarint;
-  uint32_t size = 0, ip = 0;
+  size = 0;
+  ip = 0;
   for (uint32_t i = 0; i < 5; ++i) {
     if (i >= N) break;
-    uint32_t bt = readlane(hb, i);
+    const uint32_t bt = readlane(hb, i);
     if (i < 4) {
       size |= (bt & 0x7f) << (7 * i);
       if (bt < 0x80) {
@@ -561,6 +553,22 @@ __global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
       }
     }
   }
+  return st;
+}
+
+__global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[kWalkLevels * 256];  // tag-walk jump tables
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];                // output window
+  const uint32_t b = blockIdx.x;
+  const uint32_t lane = lane_id();
+  const uint8_t* in = a.in + a.in_off[b];
+  const uint32_t N = a.in_len[b];
+  uint8_t* dst = a.out + a.out_off[b];
+  const uint32_t cap = a.out_cap[b];
+
+  uint32_t size = 0, ip = 0;
+  int32_t st = parse_header(in, N, lane, size, ip);
   if (st == kOk && size > cap) st = kBufferTooSmall;
   if (st == kOk) {
     uint32_t op_end = 0;
@@ -580,8 +588,9 @@ __global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
 // does not index:
 //  1. k_stream_index, one wave per 4 KiB chunk of the compressed body: the wave walks the tags
 //     speculatively from the chunk's first byte (walk_window, 256 bytes per step: "lane 0's
-//     path"), recording each visited position and the output before it; lanes l = 1..63 walk from byte l until they meet lane 0's path (tag walks
-//     resynchronise within a few tags on compressible data) or leave the chunk.  Each chunk then
+//     path"), recording each visited position and the output before it; lanes l = 1..63 walk
+//     from byte l (window-wise pointer doubling, the path's positions as stop nodes) until they
+//     meet lane 0's path (tag walks resynchronise) or leave the chunk.  Each chunk then
 //     knows, for entry offsets 0..63, where the walk leaves it and how much output it makes.
 //  2. The host chains the true path (sm_api.hip) and locates each fragment's chunk.
 //  3. k_decompress_frags, one wave per fragment: walk (window-parallel) from the chunk entry to
@@ -628,7 +637,8 @@ __device__ inline void stage_bytes(uint8_t* buf, const uint8_t* __restrict__ in,
         w[u] = __builtin_amdgcn_alignbyte(src[k + 1], src[k], mis);
       } else {
         uint32_t v = 0;
-        for (uint32_t j = 0; j < 4; ++j) v |= (b + j < N ? (uint32_t)in[b + j] : 0u) << (8 * j);
+        if (k < nw)
+          for (uint32_t j = 0; j < 4; ++j) v |= (b + j < N ? (uint32_t)in[b + j] : 0u) << (8 * j);
         w[u] = v;
       }
     }
@@ -818,6 +828,104 @@ __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __res
     if (st == kOk && op_end != (fr.lim == 0xffffffffu ? size : fr.lim)) st = kErrCross;
   }
   if (lane == 0) status[f] = st;
+}
+
+// ---- validation and declared lengths, no output -----------------------
+// k_validate: the decoder's tag walk and checks (decode_stream_batch, internal.jl:411-527)
+// without moving data: a block's status is exactly what uncompress(block) returns with an
+// unlimited output buffer (snappy-c.h snappy_validate_compressed_buffer).  One wave per block,
+// a 256-byte window per step, staged from HBM into LDS.
+__global__ __launch_bounds__(64) void k_validate(const uint8_t* __restrict__ d_in, const uint64_t* in_off,
+                                                 const uint32_t* in_len, int32_t* status) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[320];
+  __shared__ __attribute__((aligned(16))) uint16_t jt[kWalkLevels * 256];
+  const uint32_t b = blockIdx.x, lane = lane_id();
+  const uint8_t* in = d_in + in_off[b];
+  const uint32_t N = in_len[b];
+  uint32_t size, ip;
+  int32_t st = parse_header(in, N, lane, size, ip);
+  uint64_t op = 0, p = ip;
+  const uint64_t lim = N ? N - 1 : 0;  // tags start below N-1 (:416)
+  while (st == kOk && p < lim) {
+    stage_bytes(buf, in, N, (uint32_t)p, 320, lane);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    uint32_t rel, next, ob, excl;
+    const uint32_t ntok = window_tags(buf, 0, (uint32_t)min(lim - p, (uint64_t)256), jt, lane, rel, next, ob, excl);
+    const bool mine = lane < ntok || (ntok == 0 && lane == 0);  // ntok == 0: a long literal at p
+    const uint64_t hv = lds_ld64(buf, mine ? rel : 0u);
+    const uint32_t c = (uint32_t)hv & 0xff;
+    const uint32_t entry = char_entry(c);
+    const uint32_t len = entry & 0xff;
+    const uint32_t taglen = entry >> 11;
+    const uint32_t tr_raw = (uint32_t)(hv >> 8);
+    const uint32_t trailer = taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * taglen)) - 1u));
+    const uint32_t offset = (entry & 0x700) + trailer;
+    const uint32_t litlen = len + trailer;  // u32 wrap, as the reference
+    const uint64_t opt = op + (ntok ? excl : 0u);
+    const int64_t avail_out = (int64_t)size - (int64_t)opt;
+    int32_t err = kOk;
+    if (mine) {
+      if (c & 3) {
+        if ((int64_t)opt <= (int64_t)(uint32_t)(offset - 1u)) err = kErrCopyOffset;                                  // :499
+        else if (!(len <= 16 && offset >= 8 && avail_out >= 16) && avail_out < (int64_t)len) err = kErrCopyLength;  // :505
+      } else {
+        const int64_t avail_in = (int64_t)N - (int64_t)(p + (ntok ? rel : 0u) + 1 + taglen);
+        if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) err = kErrLiteral;  // :518
+      }
+    }
+    const uint64_t em = ballot(err != kOk);
+    if (em) {
+      st = (int32_t)readlane((uint32_t)err, ctz64(em));
+      break;
+    }
+    if (ntok == 0) {
+      op += readlane(litlen, 0);
+      p += 1 + readlane(taglen, 0) + (uint64_t)readlane(litlen, 0);
+    } else {
+      op += readlane(excl + ob, ntok - 1);
+      p += readlane(next, ntok - 1);
+    }
+  }
+  if (st == kOk && op != size) st = kErrInvalid;  // Snappy.jl:50
+  if (lane == 0) status[b] = st;
+}
+
+// k_uncompressed_length: the varint header of each block (length_uncompressed,
+// src/Snappy.jl:90-92), one thread per block
+__global__ __launch_bounds__(256) void k_uncompressed_length(const uint8_t* __restrict__ d_in, const uint64_t* in_off,
+                                                             const uint32_t* in_len, uint32_t nblk, uint32_t* out_len,
+                                                             int32_t* status) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nblk) return;
+  const uint8_t* in = d_in + in_off[b];
+  const uint32_t N = in_len[b];
+  uint32_t v = 0;
+  int32_t st = kErrVarint;
+  for (uint32_t i = 0; i < 5 && i < N; ++i) {
+    const uint32_t bt = in[i];
+    v |= (bt & 0x7f) << (7 * i);
+    if (i < 4 ? bt < 0x80 : bt < 0x10) {
+      st = kOk;
+      break;
+    }
+  }
+  out_len[b] = st == kOk ? v : 0;
+  status[b] = st;
+}
+
+hipError_t launch_validate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t nblk,
+                           int32_t* status, hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_validate, dim3(nblk), dim3(64), 0, s, in, in_off, in_len, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_uncompressed_length(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                      uint32_t nblk, uint32_t* out_len, int32_t* status, hipStream_t s) {
+  if (nblk == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_uncompressed_length, dim3((nblk + 255) / 256), dim3(256), 0, s, in, in_off, in_len, nblk,
+                     out_len, status);
+  return hipGetLastError();
 }
 
 hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec_exit,

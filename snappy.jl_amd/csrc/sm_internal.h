@@ -48,6 +48,10 @@ struct StreamFrag {
   uint32_t F;    // the fragment's first output position (a multiple of 65536)
   uint32_t lim;  // output limit (0xffffffff for the last fragment: parse to the end)
 };
+hipError_t launch_validate(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len, uint32_t nblk,
+                           int32_t* status, hipStream_t s);
+hipError_t launch_uncompressed_length(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
+                                      uint32_t nblk, uint32_t* out_len, int32_t* status, hipStream_t s);
 hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec_exit,
                                uint32_t* rec_out, hipStream_t s);
 hipError_t launch_decompress_frags(const uint8_t* in, uint32_t N, uint32_t size, uint8_t* out,

@@ -182,14 +182,13 @@ def test_decompress_leniencies(sm, gpu_available, oracle):
     assert _status(sm, bytes([0x40, 0x12, 0x00, 0x00]))[0] == 19
 
 
-def test_decompress_mutation_fuzz_batched(sm, oracle, gpu_available):
-    """Seeded byte flips / truncations / extensions of valid streams: identical status codes
-    (first error in stream order) and outputs vs the oracle, decoded as one GPU batch."""
-    rng = np.random.default_rng(1234)
+def _fuzz_cases(oracle, count, seed):
+    """Seeded byte flips / truncations / extensions of valid streams."""
+    rng = np.random.default_rng(seed)
     base = [oracle.compress(read_testfile(f)[:4096]) for f in ("html", "alice29.txt", "kppkn.gtb", "urls.10K")]
     base += [oracle.compress(b"ab" * 700), oracle.compress(bytes(range(256)) * 3)]
     cases = []
-    for i in range(3000):
+    for i in range(count):
         s = bytearray(base[i % len(base)])
         kind = rng.integers(0, 4)
         if kind == 0:
@@ -204,6 +203,13 @@ def test_decompress_mutation_fuzz_batched(sm, oracle, gpu_available):
             s[p] = int(rng.integers(0, 256))
             s = s[: max(1, len(s) - int(rng.integers(0, 8)))]
         cases.append(bytes(s))
+    return cases
+
+
+def test_decompress_mutation_fuzz_batched(sm, oracle, gpu_available):
+    """Seeded byte flips / truncations / extensions of valid streams: identical status codes
+    (first error in stream order) and outputs vs the oracle, decoded as one GPU batch."""
+    cases = _fuzz_cases(oracle, 3000, 1234)
     caps = []
     for c in cases:
         try:
@@ -323,3 +329,69 @@ def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
         assert st_g == st_o
         if st_o == 0:
             assert out_g == out_o
+
+
+def _device_batch(streams):
+    import torch
+    dev = torch.device("cuda", 0)
+    buf, in_off, in_len = _pack(streams)
+    return (torch.from_numpy(buf).to(dev), torch.from_numpy(in_off.astype(np.int64)).to(dev),
+            torch.from_numpy(in_len.astype(np.int32)).to(dev))
+
+
+def _pack(streams):
+    lens = np.array([len(x) for x in streams], dtype=np.uint32)
+    offs = np.zeros(len(streams), dtype=np.uint64)
+    if len(streams) > 1:
+        offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    buf = np.frombuffer(b"".join(streams) + b"\0" * 16, dtype=np.uint8).copy()
+    return buf, offs, lens
+
+
+def _validate_statuses(sm, streams):
+    import torch
+    d_in, d_off, d_len = _device_batch(streams)
+    d_st = torch.full((len(streams),), -1, dtype=torch.int32, device=d_in.device)
+    sm.validate_batch_device(d_in, d_off, d_len, d_st)
+    torch.cuda.synchronize()
+    return d_st.cpu().numpy()
+
+
+def test_validate_batch_matches_oracle(sm, oracle, gpu_available):
+    """sm_validate_batch_device: the status uncompress() would return,
+    without output -- corrupted, fuzzed, leniency and valid streams vs the oracle's decoder."""
+    from test_oracle import corrupted_cases
+    import streams as S
+    rng = np.random.default_rng(77)
+    cases = list(corrupted_cases(oracle)) + _fuzz_cases(oracle, 2000, 4321)
+    cases += [oracle.compress(read_testfile(f)) for f in ("html", "alice29.txt", "fireworks.jpeg", "urls.10K")]
+    cases += [S.build(S.random_ops(rng, 20000, long_lit_p=0.2))[0] for _ in range(20)]
+    good = oracle.compress(b"hello hello hello hello")
+    cases += [good + b"\x07", b"\x00\x00", b"\x00", b"\x00\x00\x00", bytes([0x40, 0x12, 0x00, 0x00]), b"",
+              b"\xff\xff\xff\xff\x7f", b"\x80"]
+    got = _validate_statuses(sm, cases)
+    want = [oracle.uncompress_status(c)[0] for c in cases]
+    bad = [(i, int(g), w) for i, (g, w) in enumerate(zip(got, want)) if int(g) != w]
+    assert not bad, bad[:10]
+    assert sum(1 for w in want if w == 0) >= 30 and sum(1 for w in want if w != 0) >= 500
+    # the single-buffer entry point
+    for c in cases[-40:]:
+        assert sm.validate(c) == oracle.uncompress_status(c)[0]
+
+
+def test_uncompressed_length_batch_device(sm, oracle, gpu_available):
+    import torch
+    cases = [b"", b"\x00", b"\x80", b"\x7f", b"\x80\x80\x04", b"\xff\xff\xff\xff\x0f", b"\xff\xff\xff\xff\x10",
+             b"\xff\xff\xff\xff\xff\x01", oracle.compress(read_testfile("html"))]
+    cases += [oracle.encode32(1 << i) for i in range(31)]
+    d_in, d_off, d_len = _device_batch(cases)
+    d_n = torch.zeros(len(cases), dtype=torch.int32, device=d_in.device)
+    d_st = torch.full((len(cases),), -1, dtype=torch.int32, device=d_in.device)
+    sm.uncompressed_length_batch_device(d_in, d_off, d_len, d_n, d_st)
+    torch.cuda.synchronize()
+    for c, n, st in zip(cases, d_n.cpu().numpy().view(np.uint32), d_st.cpu().numpy()):
+        try:
+            want = oracle.uncompressed_length(c)
+            assert (int(st), int(n)) == (0, want), c
+        except oracle.OracleError as e:
+            assert (int(st), int(n)) == (e.code, 0), c
