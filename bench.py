@@ -47,6 +47,31 @@ def load_package():
     return mod
 
 
+# test/runtests.jl:8-24, the round-trip corpus; config 5 tiles it
+ROUNDTRIP_FILES = ["alice29.txt", "asyoulik.txt", "html", "html_x_4", "kppkn.gtb", "lcet10.txt", "fireworks.jpeg",
+                   "geo.protodata", "paper-100k.pdf", "plrabn12.txt", "urls.10K", "random1.bin", "random2.bin",
+                   "random3.bin", "smallrandom1.bin"]
+CONFIG5_BYTES = 675_282_944  # 644 MiB = exactly 10,304 blocks
+
+
+def large_corpus(nbytes=CONFIG5_BYTES, seed=0x5EED + 5):
+    """Config 5 ("large"): the 15 round-trip files (4,137,377 B) tiled, each tile rotated by a
+    seeded offset, cut at nbytes.  One snappy stream of this is the single-stream workload."""
+    corpus = np.frombuffer(b"".join(open(os.path.join(TESTDATA, f), "rb").read() for f in ROUNDTRIP_FILES),
+                           dtype=np.uint8)
+    rng = np.random.default_rng(seed)
+    out = np.empty(nbytes, dtype=np.uint8)
+    pos = 0
+    while pos < nbytes:
+        r = int(rng.integers(0, len(corpus)))
+        n = min(len(corpus), nbytes - pos)
+        k = min(n, len(corpus) - r)
+        out[pos:pos + k] = corpus[r:r + k]
+        out[pos + k:pos + n] = corpus[:n - k]
+        pos += n
+    return out
+
+
 def text_blocks(nblk, seed):
     corpus = b"".join(open(os.path.join(TESTDATA, f), "rb").read() for f in TEXTS)
     arr = np.frombuffer(corpus, dtype=np.uint8)
@@ -90,6 +115,34 @@ class Batch:
         ok = bool(torch.equal(self.d_dec, self.d_in)) and int(self.status.abs().sum()) == 0
         ok = ok and bool((self.dec_len == BLOCK).all())
         return ok
+
+
+def config5_stream(sm, reps=3):
+    """Config 5 as ONE stream through the single-buffer C entry points (sm_compress /
+    sm_uncompress), host buffers allocated and touched once: PCIe-inclusive GB/s, best of reps."""
+    import ctypes
+    big = large_corpus()
+    n = big.size
+    L, ctx = sm.lib(), sm.context(0)
+    cap = sm.maxlength_compressed(n)
+    comp = np.zeros(cap, dtype=np.uint8)
+    back = np.zeros(n, dtype=np.uint8)
+    cl, bl = ctypes.c_size_t(0), ctypes.c_size_t(0)
+    tc, td = [], []
+    for _ in range(reps + 1):
+        cl.value = cap
+        t0 = time.perf_counter()
+        st = L.sm_compress(ctx, big.ctypes.data, n, comp.ctypes.data, ctypes.byref(cl), 1)
+        tc.append(time.perf_counter() - t0)
+        bl.value = n
+        t0 = time.perf_counter()
+        st2 = L.sm_uncompress(ctx, comp.ctypes.data, cl.value, back.ctypes.data, ctypes.byref(bl))
+        td.append(time.perf_counter() - t0)
+    good = st == 0 and st2 == 0 and bl.value == n and bool(np.array_equal(back, big))
+    return {"config5_stream_host_compress_GBps": round(n / min(tc[1:]) / 1e9, 3),
+            "config5_stream_host_uncompress_GBps": round(n / min(td[1:]) / 1e9, 3),
+            "config5_stream_ratio": round(cl.value / n, 5),
+            "config5_stream_ok": good and sm.last_uncompress_path() == 1}
 
 
 def time_kernel(fn, reps):
@@ -259,6 +312,10 @@ def main():
         extras["random_ratio"] = round(rb_comp / in_bytes, 5)
         t_rr = time_kernel(lambda: rb.compress(sm, "reference"), 1)
         extras["random_reference_compress_GBps"] = round(in_bytes / (t_rr * 1e-3) / 1e9, 3)
+
+    if args.extras and rank == 0:
+        extras.update(config5_stream(sm))
+        ok = ok and extras["config5_stream_ok"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

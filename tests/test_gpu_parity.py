@@ -395,3 +395,26 @@ def test_uncompressed_length_batch_device(sm, oracle, gpu_available):
             assert (int(st), int(n)) == (0, want), c
         except oracle.OracleError as e:
             assert (int(st), int(n)) == (e.code, 0), c
+
+
+def test_config5_large_stream(sm, oracle, gpu_available):
+    """SURVEY §8(d) config 5 (644 MiB = 10,304 fragments, the round-trip corpus tiled with
+    seeded rotations) as ONE stream: reference-mode bytes equal the oracle's, the parallel
+    single-stream decode restores it, and the fast-mode stream round-trips."""
+    import hashlib
+    sys_path_root()
+    import bench
+    raw = bench.large_corpus().tobytes()
+    comp = sm.compress(raw, mode="reference")
+    assert hashlib.sha256(comp).digest() == hashlib.sha256(oracle.compress(raw)).digest()
+    assert sm.uncompress(comp) == raw
+    assert sm.last_uncompress_path() == 1
+    fast = sm.compress(raw, mode="fast")
+    assert sm.uncompress(fast) == raw
+    assert sm.last_uncompress_path() == 1
+
+
+def sys_path_root():
+    import sys
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
