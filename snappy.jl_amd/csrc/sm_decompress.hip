@@ -53,7 +53,8 @@ typedef uint64_t __attribute__((aligned(1))) du64u;
 
 constexpr uint32_t kRing = 1024;
 constexpr uint32_t kMaxBatchLit = 200;  // longer literals stop a window walk (size 255)
-constexpr int kWalkLevels = 6;  // J0..J5: 63 steps = the 64 tags of a batch
+constexpr int kWalkLevels = 5;  // tables J0..J4 in LDS; J5 (bit 5 of a lane's chain index) = J4 o J4
+constexpr int kJt = kWalkLevels * 256;  // u16 jump-table entries of a walk
 constexpr int kPass = 2;        // 8-byte chunks per execution pass (most tags are <= 16 B)
 
 __device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
@@ -200,7 +201,8 @@ __device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t from
 // to the window (window end or N-1, internal.jl:416).  Every lane computes the speculative
 // sizes of its 4 positions (packed u8 in `sizes`, 255 = a literal too long for a batch).
 // J0[p] = p + size(p); a long literal or a position at/after rlim is a stop node (J0[p] = p).
-// J_k = J_{k-1} o J_{k-1}, k < kWalkLevels: 64 tags = chain elements 0..63 from position 0.
+// J_k = J_{k-1} o J_{k-1}, k < 5, in LDS (J5 = J4 o J4 is applied as two J4 reads, which
+// keeps the decoder's LDS at 7.7 KB: 20 waves per CU): 64 tags = chain elements 0..63.
 // Lane t then holds tag t directly -- J_k applied for every set bit k of t -- with its window
 // position cpos and size csz; stop nodes are fixed points, so the tags are a prefix of
 // lanes.  Returns their count.
@@ -229,6 +231,11 @@ __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt,
   for (int k = 0; k < kWalkLevels; ++k) {
     const uint32_t t = c < 256 ? jt[k * 256 + c] : c;
     c = ((lane >> k) & 1u) ? t : c;
+  }
+  if (lane >= 32) {  // J5 = J4 o J4
+    const uint16_t* j4 = jt + (kWalkLevels - 1) * 256;
+    c = c < 256 ? j4[c] : c;
+    c = c < 256 ? j4[c] : c;
   }
   // (the shuffle runs with every lane active: a ds_bpermute from an inactive lane reads 0)
   const uint32_t szw = __shfl(sizes, (c >> 2) & 63u, 64);
@@ -558,7 +565,7 @@ __device__ inline int32_t parse_header(const uint8_t* in, uint32_t N, uint32_t l
 
 __global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t sjt[kWalkLevels * 256];  // tag-walk jump tables
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];  // tag-walk jump tables
   __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];                // output window
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
@@ -668,7 +675,7 @@ __device__ inline uint32_t window_tags(const uint8_t* buf, uint32_t rel0, uint32
 __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
                                                      uint32_t* rec_exit, uint32_t* rec_out) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kIdxChunk + kIdxPad];
-  __shared__ __attribute__((aligned(16))) uint16_t jt[kWalkLevels * 256];
+  __shared__ __attribute__((aligned(16))) uint16_t jt[6 * 256];  // walk tables, then the entry walk's 3 KiB
   __shared__ uint32_t bm[kIdxChunk / 32];  // positions on lane 0's path
   __shared__ uint32_t cum[kIdxChunk];      // output before each such position
   const uint32_t c = blockIdx.x, lane = lane_id();
@@ -714,7 +721,7 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
   uint32_t pre = 0, res = tot0;
   bool done = lane == 0 || SM_IDX_NOLANES;  // (SM_IDX_NOLANES: timing variant only)
   uint16_t* tj = jt;                                   // 2 x 256 u16
-  uint32_t* to = reinterpret_cast<uint32_t*>(jt + 512);  // 2 x 256 u32 (jt holds 3 KiB)
+  uint32_t* to = reinterpret_cast<uint32_t*>(jt + 512);  // 2 x 256 u32 (jt holds 3 KiB here)
   while (true) {
     bool again = true;
     while (ballot(again)) {  // settle: out of the chunk, on the path, or a long literal
@@ -786,7 +793,7 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
 __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
                                                             uint8_t* out, const StreamFrag* frags, int32_t* status) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t sjt[kWalkLevels * 256];
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];
   __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];
   __shared__ __attribute__((aligned(16))) uint8_t sbuf[kIdxChunk + kIdxPad];
   const uint32_t f = blockIdx.x, lane = lane_id();
@@ -838,7 +845,7 @@ __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __res
 __global__ __launch_bounds__(64) void k_validate(const uint8_t* __restrict__ d_in, const uint64_t* in_off,
                                                  const uint32_t* in_len, int32_t* status) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[320];
-  __shared__ __attribute__((aligned(16))) uint16_t jt[kWalkLevels * 256];
+  __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
   const uint32_t b = blockIdx.x, lane = lane_id();
   const uint8_t* in = d_in + in_off[b];
   const uint32_t N = in_len[b];
