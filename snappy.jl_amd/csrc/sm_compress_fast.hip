@@ -147,9 +147,13 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     for (uint32_t k = tid; k < n; k += kThreads) data[k] = src[k];
   }
   {
-    uint4 z = make_uint4(0, 0, 0, 0);
+    // shared table: 0 = empty; private entries: position field 0 (empty, below every insert)
+    // and an all-ones word, so a probe matches an empty entry only for the word 0xffffffff
+    // and then yields the rejected position 0xffffffff
+    const uint4 z = make_uint4(0, 0, 0, 0), e = make_uint4(0xffffffffu, 0, 0xffffffffu, 0);
     uint4* t16 = reinterpret_cast<uint4*>(T);
-    for (uint32_t k = tid; k < (kFTab + 2 * kWavesPerBlock * kPriv) / 4; k += kThreads) t16[k] = z;
+    for (uint32_t k = tid; k < kFTab / 4; k += kThreads) t16[k] = z;
+    for (uint32_t k = kFTab / 4 + tid; k < (kFTab + 2 * kWavesPerBlock * kPriv) / 4; k += kThreads) t16[k] = e;
   }
   uint32_t op = 0;
   if (a.header) {
@@ -221,13 +225,16 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         const uint32_t cb = t1[j] != 0 ? t1[j] - 1 : q;
         uint32_t cc = q;
         if (kNbr) {
+          // wave w-m's table; for m > w the index wraps to a later chunk of the round, whose
+          // positions fail cc < q below and whose older entries are genuine earlier matches
           const uint32_t hp = ((uint32_t)wq * kHashMul) >> (32 - kPrivBits);
+          const uint64_t* P0 = reinterpret_cast<const uint64_t*>(T + kFTab);
           uint64_t v[kNbr ? kNbr : 1];
 #pragma unroll
-          for (uint32_t m = 1; m <= kNbr; ++m) v[m - 1] = m <= wave ? P[hp - m * kPriv] : 0ull;
+          for (uint32_t m = 1; m <= kNbr; ++m) v[m - 1] = P0[((wave - m) & (kWavesPerBlock - 1)) * kPriv + hp];
 #pragma unroll
           for (int m = (int)kNbr; m >= 1; --m)
-            cc = ((v[m - 1] >> 32) != 0 && (uint32_t)v[m - 1] == (uint32_t)wq) ? (uint32_t)(v[m - 1] >> 32) - 1 : cc;
+            cc = (uint32_t)v[m - 1] == (uint32_t)wq ? (uint32_t)(v[m - 1] >> 32) - 1 : cc;
         }
         // verify 4 bytes, then grow to 8 and 16; every read is masked to the lanes still
         // matching (an LDS access costs by its active lanes)
