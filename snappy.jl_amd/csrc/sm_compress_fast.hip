@@ -51,6 +51,7 @@ constexpr uint32_t kChunk = 128;
 constexpr uint32_t kWavesPerBlock = SM_FAST_WAVES;  // 16: four waves per SIMD hide the LDS latency chain
 constexpr uint32_t kThreads = 64 * kWavesPerBlock;
 constexpr uint32_t kLevels = 5;              // J0..J4: the copy-to-copy walk of a chunk takes <= 31 steps
+constexpr uint32_t kRow = kChunk + 8;        // a jump-table row (8-B aligned); entry kChunk, the chunk end, is its own image
 constexpr uint32_t kEager = 16;               // bytes compared per candidate before the long-match loop
 #ifndef SM_FAST_NBR
 #define SM_FAST_NBR 6
@@ -116,7 +117,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   const uint32_t lane = tid & 63;
   uint64_t* P = reinterpret_cast<uint64_t*>(T + kFTab) + wave * kPriv;       // private table
   uint32_t* csize = T + kFTab + 2 * kWavesPerBlock * kPriv;                   // per-wave chunk sizes
-  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + kWavesPerBlock) + wave * kLevels * kChunk;  // parse jump tables
+  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + kWavesPerBlock) + wave * kLevels * kRow;  // parse jump tables
 
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.in_len[b];
@@ -155,6 +156,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     for (uint32_t k = tid; k < kFTab / 4; k += kThreads) t16[k] = z;
     for (uint32_t k = kFTab / 4 + tid; k < (kFTab + 2 * kWavesPerBlock * kPriv) / 4; k += kThreads) t16[k] = e;
   }
+  if (lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
   uint32_t op = 0;
   if (a.header) {
     uint32_t nb = varint_len(n);
@@ -314,8 +316,8 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            jv[j] = jv[j] < kChunk ? jt[(k - 1) * kChunk + jv[j]] : jv[j];
-            jt[k * kChunk + 64 * j + lane] = (uint8_t)jv[j];
+            jv[j] = jt[(k - 1) * kRow + jv[j]];
+            jt[k * kRow + 64 * j + lane] = (uint8_t)jv[j];
           }
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         uint32_t c = 0;
 #pragma unroll
         for (int k = 0; k < (int)kLevels; ++k) {
-          const uint32_t t = c < kChunk ? jt[k * kChunk + c] : c;
+          const uint32_t t = jt[k * kRow + c];
           c = ((lane >> k) & 1u) ? t : c;
         }
         // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles
@@ -491,7 +493,7 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 #endif
 
 constexpr size_t kFastLds =
-    kBlockSize + 4 * (kFTab + 2 * kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * kLevels * kChunk;
+    kBlockSize + 4 * (kFTab + 2 * kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * kLevels * kRow;
 static_assert(kFastLds <= 160 * 1024, "fast compressor LDS exceeds a CU");
 
 hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s) {
