@@ -54,7 +54,8 @@ typedef uint64_t __attribute__((aligned(1))) du64u;
 constexpr uint32_t kRing = 1024;
 constexpr uint32_t kMaxBatchLit = 200;  // longer literals stop a window walk (size 255)
 constexpr int kWalkLevels = 5;  // tables J0..J4 in LDS; J5 (bit 5 of a lane's chain index) = J4 o J4
-constexpr int kJt = kWalkLevels * 256;  // u16 jump-table entries of a walk
+constexpr int kJtRow = 264;             // a jump-table row (u16): positions 0..255, then 256 = beyond the window
+constexpr int kJt = kWalkLevels * kJtRow;  // u16 jump-table entries of a walk
 constexpr int kPass = 2;        // 8-byte chunks per execution pass (most tags are <= 16 B)
 
 __device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
@@ -200,7 +201,8 @@ __device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t from
 // cw = the 8 stream bytes at window position 4*lane; rlim (<= 256) = the parse limit relative
 // to the window (window end or N-1, internal.jl:416).  Every lane computes the speculative
 // sizes of its 4 positions (packed u8 in `sizes`, 255 = a literal too long for a batch).
-// J0[p] = p + size(p); a long literal or a position at/after rlim is a stop node (J0[p] = p).
+// J0[p] = p + size(p), clamped to 256 (beyond the window; its row entry maps to itself, so no
+// read is conditional); a long literal or a position at/after rlim is a stop node (J0[p] = p).
 // J_k = J_{k-1} o J_{k-1}, k < 5, in LDS (J5 = J4 o J4 is applied as two J4 reads, which
 // keeps the decoder's LDS at 7.7 KB: 20 waves per CU): 64 tags = chain elements 0..63.
 // Lane t then holds tag t directly -- J_k applied for every set bit k of t -- with its window
@@ -214,28 +216,29 @@ __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt,
   for (int j = 0; j < 4; ++j) {
     const uint32_t p = 4 * lane + j;
     const uint32_t sz = (sizes >> (8 * j)) & 0xff;
-    J[j] = (sz == 255 || p >= rlim) ? p : p + sz;
+    J[j] = (sz == 255 || p >= rlim) ? p : min(p + sz, 256u);  // 256: beyond the window
   }
+  if (lane < kWalkLevels) jt[lane * kJtRow + 256] = 256;  // every row maps 256 to itself
   *reinterpret_cast<uint2*>(jt + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
 #pragma unroll
   for (int k = 1; k < kWalkLevels; ++k) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint16_t* prev = jt + (k - 1) * 256;
+    const uint16_t* prev = jt + (k - 1) * kJtRow;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) J[j] = J[j] < 256 ? prev[J[j]] : J[j];
-    *reinterpret_cast<uint2*>(jt + k * 256 + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+    for (int j = 0; j < 4; ++j) J[j] = prev[J[j]];
+    *reinterpret_cast<uint2*>(jt + k * kJtRow + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
   }
   __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the u16 reads below follow the uint2 stores
   uint32_t c = 0;
 #pragma unroll
   for (int k = 0; k < kWalkLevels; ++k) {
-    const uint32_t t = c < 256 ? jt[k * 256 + c] : c;
+    const uint32_t t = jt[k * kJtRow + c];
     c = ((lane >> k) & 1u) ? t : c;
   }
   if (lane >= 32) {  // J5 = J4 o J4
-    const uint16_t* j4 = jt + (kWalkLevels - 1) * 256;
-    c = c < 256 ? j4[c] : c;
-    c = c < 256 ? j4[c] : c;
+    const uint16_t* j4 = jt + (kWalkLevels - 1) * kJtRow;
+    c = j4[c];
+    c = j4[c];
   }
   // (the shuffle runs with every lane active: a ds_bpermute from an inactive lane reads 0)
   const uint32_t szw = __shfl(sizes, (c >> 2) & 63u, 64);
