@@ -43,9 +43,9 @@
 namespace sm {
 
 #if SM_STAMP
-__device__ unsigned long long g_stamp[8];
+__device__ unsigned long long g_stamp[10];
 #endif
-STAMP_MACROS(8)
+STAMP_MACROS(10)
 
 typedef uint16_t __attribute__((aligned(1))) du16u;
 typedef uint32_t __attribute__((aligned(1))) du32u;
@@ -437,6 +437,8 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         }
         done |= rm;
       }
+      STAMP(8)
+      STAMP_COUNT(9, __builtin_popcountll(~done))
       // The copies left (a few per batch: their source overlaps earlier tags of this batch) run
       // in stream order, one tag at a time, a byte per lane: byte k = S[k mod offset] with S
       // final by then (LDS accesses of a wave are serviced in order).
@@ -962,7 +964,7 @@ hipError_t launch_decompress(const DecompressArgs& a, int /*large*/, hipStream_t
 extern "C" int sm_debug_stamps(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(g_stamp)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[10] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z)) != hipSuccess) return -1;
   }
   return 0;

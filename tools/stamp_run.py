@@ -5,9 +5,10 @@ Build the diagnostic library, then run:
       snappy.jl_amd/csrc/sm_*.hip
   SNAPPY_MI355X_LIB=tools/abl/lib_stamp.so python3 tools/stamp_run.py [--data text|random]
   ... --op compress_fast: the fast compressor's per-round sections instead.
-Decoder sections (per wave, summed over all streams): 0 ring management, 1 tag walk (sizes, doubling,
-descent, compaction), 2 per-tag decode + error checks, 3 dependency search + long literals,
-4 execution rounds, 5 prefetch issue + big literals + tail; 6 = batches, 7 = rounds.
+Decoder sections (per wave, summed over all streams): 0 flush + ring management, 1 tag walk,
+2 per-tag decode + error checks, 3 long literals, 8 the execution round, 4 the in-order tail
+(copies whose source is in the batch), 5 big literals; counters 6 = batches, 7 = rounds +
+in-order tags, 9 = in-order tags.
 """
 import argparse
 import ctypes
@@ -20,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
-NAMES = ["ring", "walk", "decode", "deps+longlit", "rounds", "prefetch+big+tail"]
+NAMES = ["ring+flush", "walk", "decode", "longlit", "in-order tail", "big literals", "", "", "round"]
 CNAMES = ["inserts", "B1 wait", "candidates", "long matches", "parse", "tokens+sizes", "prefetch",
           "B2 wait", "layout", "emission", "tail"]
 
@@ -46,19 +47,21 @@ def main():
     b.compress(sm, "fast")
     b.uncompress(sm)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 10)()
     fn(buf, 1)
     for _ in range(args.reps):
         b.uncompress(sm)
     torch.cuda.synchronize()
     fn(buf, 1)
     v = list(buf)
-    tot = sum(v[:6])
+    tot = sum(v[:6]) + v[8]
     batches, rounds = v[6], v[7]
-    print("data %s: %d batches (%.1f per block), %d rounds (%.2f per batch)" % (
-        args.data, batches, batches / args.blocks / args.reps, rounds, rounds / max(batches, 1)))
+    print("data %s: %d batches (%.1f per block), %d rounds (%.2f per batch), %.2f in-order tags per batch" % (
+        args.data, batches, batches / args.blocks / args.reps, rounds, rounds / max(batches, 1),
+        v[9] / max(batches, 1)))
     for i, nme in enumerate(NAMES):
-        print("  %-18s %5.1f%%  %8.0f cycles/batch" % (nme, 100.0 * v[i] / tot, v[i] / max(batches, 1)))
+        if nme:
+            print("  %-18s %5.1f%%  %8.0f cycles/batch" % (nme, 100.0 * v[i] / tot, v[i] / max(batches, 1)))
     print("  total              %8.0f cycles/batch" % (tot / max(batches, 1)))
     print("roundtrip ok:", b.verify())
 
