@@ -32,7 +32,7 @@
 #include "sm_device.h"
 #include "sm_internal.h"
 
-#ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only)
+#ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only), 4 = no HBM sources (timing only)
 #define SM_ABLATE_D 0
 #endif
 
@@ -349,7 +349,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const uint32_t O0 = op;
       const uint32_t slo = opt - offset;
       const uint32_t shi = slo + min(len, offset);
-      const bool gsrc = iscopy && offset > kLdsSrc;  // source older than the window: from HBM
+      const bool gsrc = !(SM_ABLATE_D & 4) && iscopy && offset > kLdsSrc;  // source older than the window: from HBM
       const uint64_t all = nt == 64 ? ~0ull : ((1ull << nt) - 1);
       const bool longlit = !iscopy && litlen > 64;
       uint64_t done = (ballot(longlit) & all) | ~all;
