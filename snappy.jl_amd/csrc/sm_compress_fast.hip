@@ -4,30 +4,28 @@
 // uncompress, src/internal.jl:411-466) with a wave-parallel parse instead of the reference's
 // serial greedy loop (internal.jl:127-250).
 //
-// One workgroup of W = 16 waves per block (four per SIMD, to hide the chain of LDS round
-// trips); the block is staged once in LDS (64 KiB) beside a shared 16 K-entry latest-position
-// table (u32, 64 KiB), a 128-entry u64 private table per wave (16 KiB) and 5-level parse jump
-// tables (10 KiB): 154 KiB, one block per CU.  The block is cut into 128-byte chunks whose
-// parse never crosses the chunk end (copies are truncated there, literal runs end there), so
-// the chunks of a round are parsed independently: in round r wave w owns chunk W*r+w, two
-// positions per lane (q = c0 + 64*j + lane).  Per chunk:
-//  1. (a) insert every position into the shared table with ds_max_u32 (order-independent ->
-//     deterministic) and into the wave's private table with ds_max_rtn_u32, whose return is
-//     the latest EARLIER position of the chunk with the same 7-bit hash (lanes of one
-//     instruction are serialised in ascending order on gfx950; verified, see tools/probe_lds);
-//  2. (b) two candidates per position: A = that intra-chunk position, else the shared
-//     table after the round (if it is an earlier position); B = the shared table as of the
-//     previous round.  Both verified (4 bytes) and extended 16 bytes branch-free with unaligned
-//     ds_read_b64; the longer one wins;
-//  3. greedy parse by pointer doubling over the chunk (J_k = J_{k-1} o J_{k-1}, binary
-//     descent); the visited copies are compacted into token lanes; sizes in closed form,
-//     DPP wave scan, chunk sizes exchanged through LDS -> exact output offsets;
-//  4. (c) token lanes write tag bytes; position lanes scatter literal bytes.
-// Two barriers per round.  Output is deterministic (no order-dependent table state).
+// One workgroup of 16 waves per block, in two roles:
+//  * the INSERTER (wave 15) walks the block's positions in order, 64 per instruction, through
+//    a 16 K-entry hash table with ds_wrxchg_rtn_b32.  A wave's LDS instructions execute in
+//    order and the conflicting lanes of one instruction in ascending lane order, so the value
+//    each position gets back is exactly the sequential one: the latest and the second-latest
+//    earlier position with the same hash (a table entry holds both: the exchange puts the new
+//    position in the low half and a ds_write_b16 moves the old latest into the high half).
+//    Correctness never depends on that order -- every candidate is verified -- only the ratio
+//    does.  The candidates go to a per-round LDS ring, one round ahead of the parse.
+//  * 15 PARSE waves.  The block is cut into 128-byte chunks whose parse never crosses the chunk
+//    end (copies are truncated there, literal runs end there), so the chunks of a round are
+//    parsed independently: in round r parse wave w owns chunk 15r+w, two positions per lane.
+//    Per chunk: verify and extend the 1-2 chain candidates of every position, greedy parse by
+//    pointer doubling (J_k = J_{k-1} o J_{k-1}), token sizes in closed form and a DPP scan,
+//    then (after the round barrier) the round layout over the 15 chunks -- literal runs that
+//    cross chunk boundaries are merged -- and the emission: token lanes write tag bytes,
+//    position lanes scatter literal bytes.
+// One barrier per round (chunk infos are double-buffered).  Output is deterministic.
 #include "sm_device.h"
 #include "sm_internal.h"
 
-#ifndef SM_ABLATE  // diagnostic builds only (tools/ablate.sh): 1 no emit, 2 no matches, 4 no inserts
+#ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches
 #define SM_ABLATE 0
 #endif
 
@@ -39,24 +37,21 @@ __device__ unsigned long long g_stamp_c[12];
 STAMP_MACROS(12)
 
 constexpr uint32_t kFTabBits = 14;
-constexpr uint32_t kFTab = 1u << kFTabBits;   // shared table entries
-constexpr uint32_t kPrivBits = 7;
-constexpr uint32_t kPriv = 1u << kPrivBits;   // private (intra-chunk) table entries per wave
-// A private entry is u64 (pos+1) << 32 | the 4 bytes at pos: ds_max still orders by position,
-// and a candidate taken from it is verified in registers, with no data read.
+constexpr uint32_t kFTab = 1u << kFTabBits;   // hash table entries: u32 = (second-latest+1) << 16 | (latest+1)
 constexpr uint32_t kChunk = 128;
-#ifndef SM_FAST_WAVES
-#define SM_FAST_WAVES 16
-#endif
-constexpr uint32_t kWavesPerBlock = SM_FAST_WAVES;  // 16: four waves per SIMD hide the LDS latency chain
+constexpr uint32_t kWavesPerBlock = 16;
+constexpr uint32_t kPW = kWavesPerBlock - 1;  // parse waves; wave kPW is the inserter
 constexpr uint32_t kThreads = 64 * kWavesPerBlock;
-constexpr uint32_t kLevels = 5;              // J0..J4: the copy-to-copy walk of a chunk takes <= 31 steps
-constexpr uint32_t kRow = kChunk + 8;        // a jump-table row (8-B aligned); entry kChunk, the chunk end, is its own image
-constexpr uint32_t kEager = 16;               // bytes compared per candidate before the long-match loop
-#ifndef SM_FAST_NBR
-#define SM_FAST_NBR 6
+constexpr uint32_t kRoundPos = kPW * kChunk;  // positions per round (1920)
+constexpr uint32_t kLevels = 5;               // J0..J4: the copy-to-copy walk of a chunk takes <= 31 steps
+constexpr uint32_t kRow = kChunk + 8;         // a jump-table row (8-B aligned); entry kChunk, the chunk end, is its own image
+#ifndef SM_FAST_DEPTH
+#define SM_FAST_DEPTH 2
 #endif
-constexpr uint32_t kNbr = SM_FAST_NBR;       // earlier chunks of the round probed for candidate C
+constexpr int kDepth = SM_FAST_DEPTH;
+#ifndef SM_FAST_WALK
+#define SM_FAST_WALK 0                        // 1: scalar walk of the parse chain; 0: pointer doubling in LDS
+#endif         // chain candidates verified per position (1: latest, 2: + second-latest)
 
 // literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
 __device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
@@ -108,16 +103,56 @@ __device__ inline void put_copy_cf(uint8_t* dst, uint32_t o, uint32_t off, uint3
   }
 }
 
+#ifndef SM_FAST_HASHAHEAD
+#define SM_FAST_HASHAHEAD 0  // 1: the parse waves hash positions two rounds ahead for the inserter
+#endif
+
+// Hash slot of position q for the inserter (0xffff: no 4 bytes at q, not inserted).
+__device__ inline uint32_t hash_slot(const uint8_t* data, uint32_t q, uint32_t n) {
+  return q + 4 <= n ? (lds_ld32(data, q) * kHashMul) >> (32 - kFTabBits) : 0xffffu;
+}
+
+// Inserter: positions [r0, r0 + kRoundPos) in order; ring[i] receives the candidates of
+// position r0 + i (the old table entry).  kG groups of 64 positions per step so the LDS round
+// trips overlap.
+__device__ inline void insert_round(const uint8_t* data, uint32_t* T, uint32_t* ring, uint32_t r0, uint32_t n,
+                                    uint32_t lane) {
+  constexpr int kG = 6;
+  static_assert((kRoundPos / 64) % kG == 0, "insert step");
+  if (r0 >= n) return;
+  const uint32_t ngroups = min((n - r0 + 63) >> 6, kRoundPos / 64);
+  for (uint32_t g0 = 0; g0 < ngroups; g0 += kG) {
+    uint32_t h[kG], old[kG];
+#pragma unroll
+    for (int i = 0; i < kG; ++i)
+      h[i] = SM_FAST_HASHAHEAD ? ring[64 * (g0 + i) + lane] & 0xffffu : hash_slot(data, r0 + 64 * (g0 + i) + lane, n);
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      const uint32_t q = r0 + 64 * (g0 + i) + lane;
+      old[i] = 0;
+      if (h[i] != 0xffffu && q + 4 <= n) old[i] = __hip_atomic_exchange(&T[h[i]], q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      // the old latest becomes the second-latest (the new entry's high half)
+      const uint32_t q = r0 + 64 * (g0 + i) + lane;
+      if (kDepth > 1 && h[i] != 0xffffu && q + 4 <= n) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
+      ring[64 * (g0 + i) + lane] = old[i];
+    }
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* data = smem;                                                       // 64 KiB block
-  uint32_t* T = reinterpret_cast<uint32_t*>(smem + kBlockSize);               // shared table
+  uint8_t* data = smem;                                                     // 64 KiB block
+  uint32_t* T = reinterpret_cast<uint32_t*>(smem + kBlockSize);             // hash table
+  uint32_t* ring = T + kFTab;                                               // 2 x kRoundPos candidates
+  uint32_t* csize = ring + 2 * kRoundPos;                                   // 2 x 16 chunk infos
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = uniform(tid >> 6);
   const uint32_t lane = tid & 63;
-  uint64_t* P = reinterpret_cast<uint64_t*>(T + kFTab) + wave * kPriv;       // private table
-  uint32_t* csize = T + kFTab + 2 * kWavesPerBlock * kPriv;                   // per-wave chunk sizes
-  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + kWavesPerBlock) + wave * kLevels * kRow;  // parse jump tables
+  const bool inserter = wave == kPW;
+  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + 2 * kWavesPerBlock) + (inserter ? 0 : wave) * kLevels * kRow;
 
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.in_len[b];
@@ -148,15 +183,11 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     for (uint32_t k = tid; k < n; k += kThreads) data[k] = src[k];
   }
   {
-    // shared table: 0 = empty; private entries: position field 0 (empty, below every insert)
-    // and an all-ones word, so a probe matches an empty entry only for the word 0xffffffff
-    // and then yields the rejected position 0xffffffff
-    const uint4 z = make_uint4(0, 0, 0, 0), e = make_uint4(0xffffffffu, 0, 0xffffffffu, 0);
+    const uint4 z = make_uint4(0, 0, 0, 0);
     uint4* t16 = reinterpret_cast<uint4*>(T);
-    for (uint32_t k = tid; k < kFTab / 4; k += kThreads) t16[k] = z;
-    for (uint32_t k = kFTab / 4 + tid; k < (kFTab + 2 * kWavesPerBlock * kPriv) / 4; k += kThreads) t16[k] = e;
+    for (uint32_t k = tid; k < kFTab / 4; k += kThreads) t16[k] = z;  // 0 = no position
   }
-  if (lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
+  if (!inserter && lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
   uint32_t op = 0;
   if (a.header) {
     uint32_t nb = varint_len(n);
@@ -166,119 +197,82 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   __syncthreads();
 
   const uint32_t nchunks = (n + kChunk - 1) / kChunk;
-  const uint32_t rounds = (nchunks + kWavesPerBlock - 1) / kWavesPerBlock;
+  const uint32_t rounds = (nchunks + kPW - 1) / kPW;
+#ifndef SM_FAST_PRIO
+#define SM_FAST_PRIO 3
+#endif
+  // the inserter shares a SIMD with three parse waves and gates every round: issue it first
+  if (inserter && SM_FAST_PRIO) __builtin_amdgcn_s_setprio(SM_FAST_PRIO);
+  // hash slots of rounds 0 and 1 (later rounds: two rounds ahead, by the parse waves)
+  if (SM_FAST_HASHAHEAD) {
+    for (uint32_t i = tid; i < 2 * kRoundPos; i += kThreads) ring[i] = hash_slot(data, i, n);
+    __syncthreads();
+  }
+  if (inserter) insert_round(data, T, ring, 0, n, lane);
+  __syncthreads();
 
   uint64_t w[2];  // the 8 bytes at each position
-  uint32_t t1[2];
-  {
-    const uint32_t c0 = wave * kChunk;
+  if (!inserter) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      uint32_t q = c0 + 64 * j + lane;
+      uint32_t q = wave * kChunk + 64 * j + lane;
       w[j] = lds_ld64(data, q < n ? q : 0);
-      t1[j] = 0;
     }
   }
 
   STAMP_DECL
   for (uint32_t r = 0; r < rounds; ++r) {
-    STAMP_COUNT(11, 1)
-    const uint32_t k = r * kWavesPerBlock + wave;
-    const bool active = k < nchunks;
+    const uint32_t k = r * kPW + wave;
+    const bool active = !inserter && k < nchunks;
     const uint32_t c0 = k * kChunk;
     const uint32_t ce = active ? min(c0 + kChunk, n) : c0;
-
-    // (a) inserts
-    uint64_t pin[2] = {0, 0};
-    if (active && !(SM_ABLATE & 4)) {
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint32_t q = c0 + 64 * j + lane;
-        const uint32_t hm = (uint32_t)w[j] * kHashMul;
-        if (q + 4 <= n) {
-          __hip_atomic_fetch_max(&T[hm >> (32 - kFTabBits)], q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          pin[j] = __hip_atomic_fetch_max(&P[hm >> (32 - kPrivBits)], ((uint64_t)(q + 1) << 32) | (uint32_t)w[j],
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-    }
-    STAMP(0)
-    __syncthreads();  // B1
-    STAMP(1)
-
-    // (b) candidates, verify, extend, walk, sizes
+    uint32_t* cinfo = csize + (r & 1) * kWavesPerBlock;
     uint32_t ta = 0, tb = 0, ntok = 0, incl = 0, sz = 0, litlen = 0, littag = 0, ls = 0;
-    uint64_t ts0 = 0, ts1 = 0;
-    if (active) {
-      // Candidates per position: A = the latest earlier position of the chunk with the same
-      // 7-bit hash (ds_max_rtn above), B = the shared table as of the previous round, C = the
-      // nearest earlier chunk of this round (waves wave-1..wave-kNbr) whose private table holds
-      // a 4-byte match (the positions the round-lagged shared table misses).  The longest
-      // match wins (ties: A, B, C).
+    uint64_t ts0 = 0, ts1 = 0, wn[2] = {0, 0};
+
+    if (inserter) {
+      insert_round(data, T, ring + ((r + 1) & 1) * kRoundPos, (r + 1) * kRoundPos, n, lane);
+      STAMP(8)
+      STAMP_COUNT(10, 1)
+    } else if (active) {
+      STAMP_COUNT(11, 1)
+      // (a) candidates: the latest (and second-latest) earlier position with the same hash,
+      // verified and extended 8 bytes at a time; the longest wins (ties: the latest).
+      uint32_t* cr = ring + (r & 1) * kRoundPos + wave * kChunk;
       uint32_t Ls[2], offs[2];
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t q = c0 + 64 * j + lane;
         const bool can = q + 4 <= ce;
-        const uint64_t wq = w[j];
-        const uint32_t pa = (uint32_t)(pin[j] >> 32);
-        const bool oka = pa > c0 && (uint32_t)pin[j] == (uint32_t)wq;  // an earlier chunk position
-        const uint32_t ca = oka ? pa - 1 : q;
-        const uint32_t cb = t1[j] != 0 ? t1[j] - 1 : q;
-        uint32_t cc = q;
-        if (kNbr) {
-          // wave w-m's table; for m > w the index wraps to a later chunk of the round, whose
-          // positions fail cc < q below and whose older entries are genuine earlier matches
-          const uint32_t hp = ((uint32_t)wq * kHashMul) >> (32 - kPrivBits);
-          const uint64_t* P0 = reinterpret_cast<const uint64_t*>(T + kFTab);
-          uint64_t v[kNbr ? kNbr : 1];
+        const uint32_t cv = cr[64 * j + lane];
+        uint32_t L = 0, c = q;
 #pragma unroll
-          for (uint32_t m = 1; m <= kNbr; ++m) v[m - 1] = P0[((wave - m) & (kWavesPerBlock - 1)) * kPriv + hp];
-#pragma unroll
-          for (int m = (int)kNbr; m >= 1; --m)
-            cc = (uint32_t)v[m - 1] == (uint32_t)wq ? (uint32_t)(v[m - 1] >> 32) - 1 : cc;
-        }
-        // verify 4 bytes, then grow to 8 and 16; every read is masked to the lanes still
-        // matching (an LDS access costs by its active lanes)
-        const uint32_t cand[3] = {ca, cb, cc};
-        uint32_t len[3];
-        len[0] = (can && oka) ? 4u : 0u;                                   // verified by its entry
-        len[1] = (can && cb < q && cb != ca && lds_ld32(data, cb) == (uint32_t)wq) ? 4u : 0u;
-        len[2] = (can && cc < q && cc != ca && cc != cb) ? 4u : 0u;  // verified by the probe
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-          if (len[i]) {
-            const uint32_t x = lds_ld32(data, cand[i] + 4) ^ (uint32_t)(wq >> 32);
-            len[i] = x ? 4 + ((uint32_t)__builtin_ctz(x) >> 3) : 8u;
-          }
-        }
-        if (len[0] == 8 || len[1] == 8 || len[2] == 8) {
-          const uint64_t wq2 = lds_ld64(data, q + 8);
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            if (len[i] == 8) {
-              const uint64_t x = lds_ld64(data, cand[i] + 8) ^ wq2;
-              len[i] = x ? 8 + (uint32_t)(__builtin_ctzll(x) >> 3) : 16u;
+        for (int i = 0; i < kDepth; ++i) {
+          const uint32_t p = (cv >> (16 * i)) & 0xffffu;  // position + 1, 0 = none
+          if (can && p != 0 && p - 1 < q) {
+            const uint64_t x = lds_ld64(data, p - 1) ^ w[j];
+            const uint32_t l = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
+            if (l >= 4 && l > L) {
+              L = l;
+              c = p - 1;
             }
           }
         }
-        uint32_t L = len[0], c = ca;
-#pragma unroll
-        for (int i = 1; i < 3; ++i) {
-          c = len[i] > L ? cand[i] : c;
-          L = len[i] > L ? len[i] : L;
-        }
-        L = min(L, ce - q);
-        Ls[j] = (SM_ABLATE & 2) ? 0u : L;
+        Ls[j] = min(L, ce - q);
         offs[j] = q - c;
       }
-      STAMP(2)
-      // finish matches that filled the eager window: 8 bytes per lane per step
+      // this slot's next use: the hash slots of the same chunk index two rounds ahead
+      if (SM_FAST_HASHAHEAD) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) cr[64 * j + lane] = hash_slot(data, c0 + 2 * kRoundPos + 64 * j + lane, n);
+      }
+      STAMP(0)
+      // finish matches that filled the 8-byte window: 8 bytes per lane per step
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t q = c0 + 64 * j + lane;
         uint32_t L = Ls[j];
-        bool more = L >= kEager && q + L < ce;
+        bool more = L >= 8 && q + L < ce;
         while (ballot(more)) {
           if (more) {
             const uint32_t avail = ce - q - L;
@@ -288,9 +282,9 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
             more = fb == 8 && avail > 8;
           }
         }
-        Ls[j] = L;
+        Ls[j] = (SM_ABLATE & 2) ? 0u : L;
       }
-      STAMP(3)
+      STAMP(1)
       // Greedy parse by pointer doubling (no serial loop) over the chunk's 128 positions.
       // J0 skips literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a
       // non-match), else the chunk end, so the greedy walk from 0 steps only between copies
@@ -303,21 +297,47 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         uint32_t jv[2];
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const uint32_t r = 64 * j + lane;
-          const uint32_t x = r + Ls[j];  // <= 128: copies end inside the chunk
+          const uint32_t rr = 64 * j + lane;
+          const uint32_t x = rr + Ls[j];  // <= 128: copies end inside the chunk
           const uint64_t m0 = x < 64 ? M0 >> x : 0;
           const uint64_t m1 = x < 64 ? M1 : (x < 128 ? M1 >> (x - 64) : 0);
           const uint32_t b1 = x < 64 ? 64u : x;
           jv[j] = m0 ? x + (uint32_t)__builtin_ctzll(m0) : (m1 ? b1 + (uint32_t)__builtin_ctzll(m1) : kChunk);
-          jt[r] = (uint8_t)jv[j];
+#if !SM_FAST_WALK
+          jt[rr] = (uint8_t)jv[j];
+#endif
         }
+#if SM_FAST_WALK
+        // chain element t (lane t) by a scalar walk: position 0, then J0 of the previous
+        // element; the copy-start bitmask is built on the way.  Steps = copies + 1.
+        uint32_t c = kChunk;
+        {
+          uint32_t p = 0, t = 0;
+          uint64_t s0 = 0, s1 = 0;
+          while (p < kChunk) {
+            c = lane == t ? p : c;
+            const uint32_t l = p & 63u;
+            const bool hi = p >= 64;
+            const bool ism = ((hi ? M1 : M0) >> l) & 1u;
+            if (ism) {
+              if (hi) s1 |= 1ull << l;
+              else s0 |= 1ull << l;
+            }
+            const uint32_t a0 = readlane(jv[0], l), a1 = readlane(jv[1], l);
+            p = hi ? a1 : a0;
+            ++t;
+          }
+          ts0 = s0;
+          ts1 = s1;
+        }
+#else
 #pragma unroll
-        for (int k = 1; k < (int)kLevels; ++k) {
+        for (int kk = 1; kk < (int)kLevels; ++kk) {
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
 #pragma unroll
           for (int j = 0; j < 2; ++j) {
-            jv[j] = jt[(k - 1) * kRow + jv[j]];
-            jt[k * kRow + 64 * j + lane] = (uint8_t)jv[j];
+            jv[j] = jt[(kk - 1) * kRow + jv[j]];
+            jt[kk * kRow + 64 * j + lane] = (uint8_t)jv[j];
           }
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -325,10 +345,11 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         // element 0 can be a non-match (J0 jumps to match positions), the rest are the copies.
         uint32_t c = 0;
 #pragma unroll
-        for (int k = 0; k < (int)kLevels; ++k) {
-          const uint32_t t = jt[k * kRow + c];
-          c = ((lane >> k) & 1u) ? t : c;
+        for (int kk = 0; kk < (int)kLevels; ++kk) {
+          const uint32_t t = jt[kk * kRow + c];
+          c = ((lane >> kk) & 1u) ? t : c;
         }
+#endif
         // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles
         const uint32_t ci = c & 63u;
         const uint32_t l0 = __shfl(Ls[0], ci, 64), l1 = __shfl(Ls[1], ci, 64);
@@ -345,6 +366,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
           tb = tbv;
           last_end = readlane(c + Lc, nmatch - 1 + sh);
         }
+#if !SM_FAST_WALK
         // copy-start bitmask (position p of the chunk) for the literal scatter
         uint64_t* tsw = reinterpret_cast<uint64_t*>(jt);
         if (lane == 0) tsw[0] = tsw[1] = 0;
@@ -354,8 +376,9 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         ts0 = tsw[0];
         ts1 = tsw[1];
+#endif
       }
-      STAMP(4)
+      STAMP(2)
       ntok = nmatch;
       if (last_end < ce - c0) {  // trailing literal run: a token without a copy
         const bool me = lane == ntok;
@@ -377,28 +400,24 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       // literal piece | no copies at all
       const uint32_t trail = ce - c0 - last_end;
       if (lane == 0)
-        csize[wave] = readlane(incl, ntok - 1) | (readlane(litlen, 0) << 11) | (trail << 19) | ((nmatch == 0) << 27);
-    } else {
-      if (lane == 0) csize[wave] = 0;
-    }
-
-    STAMP(5)
-    // next round: words and first-chance candidates (table as of this round)
-    uint64_t wn[2];
-    uint32_t t1n[2];
-    {
-      const uint32_t k2 = k + kWavesPerBlock;
-      const uint32_t c2 = k2 * kChunk;
+        cinfo[wave] = readlane(incl, ntok - 1) | (readlane(litlen, 0) << 11) | (trail << 19) | ((nmatch == 0) << 27);
+      // next round's words
+      const uint32_t c2 = (k + kPW) * kChunk;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const uint32_t q = c2 + 64 * j + lane;
         wn[j] = lds_ld64(data, q < n ? q : 0);
-        t1n[j] = k2 < nchunks ? T[((uint32_t)wn[j] * kHashMul) >> (32 - kFTabBits)] : 0;
       }
+      STAMP(3)
+    } else {
+      if (lane == 0) cinfo[wave] = 0;
     }
-    STAMP(6)
-    __syncthreads();  // B2
-    STAMP(7)
+    __syncthreads();  // the round's chunk infos; the next round's candidates
+    if (inserter) {
+      STAMP(9)
+      continue;
+    }
+    STAMP(4)
 
     // (c) round layout, lane-parallel over the round's chunks (lane u = chunk u): a literal
     // run that crosses chunk boundaries inside the round is emitted once, with one tag for
@@ -409,15 +428,15 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     //               and its tag encodes the run length up to the end of the last piece.
     uint32_t myb, mycont, myrun, total;
     {
-      const uint32_t info = lane < kWavesPerBlock ? csize[lane] : 0u;
+      const uint32_t info = lane < kPW ? cinfo[lane] : 0u;
       const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0xffu, trl = (info >> 19) & 0xffu;
       const bool nocp = (info >> 27) & 1u;
       const uint32_t trl_prev = __shfl_up(trl, 1, 64);
-      const bool cont_in = lane > 0 && lane < kWavesPerBlock && trl_prev > 0 && lead > 0;
+      const bool cont_in = lane > 0 && lane < kPW && trl_prev > 0 && lead > 0;
       const bool mid = nocp && cont_in;
       const bool start = trl > 0 && !mid;
-      const bool cont_next = __shfl_down((uint32_t)cont_in, 1, 64) != 0 && lane + 1 < kWavesPerBlock;
-      const uint32_t cu = (r * kWavesPerBlock + lane) * kChunk;              // chunk start
+      const bool cont_next = __shfl_down((uint32_t)cont_in, 1, 64) != 0 && lane + 1 < kPW;
+      const uint32_t cu = (r * kPW + lane) * kChunk;                         // chunk start
       const uint32_t ceu = min(cu + kChunk, n);
       // the run ending in chunk u ends at cu + lead; a run starting in chunk v ends in the
       // first later chunk whose piece ends it (suffix min over lanes)
@@ -426,20 +445,20 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
 #pragma unroll
       for (uint32_t d = 1; d < kWavesPerBlock; d <<= 1) {
         const uint32_t o2 = __shfl_down(nxt, d, 64);
-        nxt = (lane + d < kWavesPerBlock && o2 < nxt) ? o2 : nxt;
+        nxt = (lane + d < kPW && o2 < nxt) ? o2 : nxt;
       }
       nxt = __shfl_down(nxt, 1, 64);                                         // first end after u
       const uint32_t endpos = __shfl(cu + lead, nxt & 63u, 64);
       const uint32_t runlen = (start && cont_next) ? endpos - (ceu - trl) : 0u;
       const uint32_t Sm = S - (cont_in ? lit_tag_bytes(lead) : 0u) +
                           (runlen ? lit_tag_bytes(runlen) - lit_tag_bytes(trl) : 0u);
-      const uint32_t inclm = scan_dpp(lane < kWavesPerBlock ? Sm : 0u);
-      total = readlane(inclm, kWavesPerBlock - 1);
+      const uint32_t inclm = scan_dpp(lane < kPW ? Sm : 0u);
+      total = readlane(inclm, kPW - 1);
       myb = readlane(inclm - Sm, wave);
       mycont = readlane((uint32_t)cont_in, wave);
       myrun = readlane(runlen, wave);
     }
-    STAMP(8)
+    STAMP(5)
     if (active && !(SM_ABLATE & 1)) {
       const uint32_t rm = mycont ? readlane(littag, 0) : 0u;                 // leading tag removed
       const uint32_t tq = c0 + (ta & 0xffff), tL = ta >> 16;
@@ -468,15 +487,12 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         below += __builtin_popcountll(ts);
       }
     }
-    STAMP(9)
+    STAMP(6)
     op += total;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      w[j] = wn[j];
-      t1[j] = t1n[j];
-    }
+    w[0] = wn[0];
+    w[1] = wn[1];
   }
-  STAMP(10)
+  STAMP(7)
   STAMP_FLUSH(g_stamp_c)
   if (tid == 0) a.out_len[b] = op;
 }
@@ -492,8 +508,7 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 }
 #endif
 
-constexpr size_t kFastLds =
-    kBlockSize + 4 * (kFTab + 2 * kWavesPerBlock * kPriv + kWavesPerBlock) + kWavesPerBlock * kLevels * kRow;
+constexpr size_t kFastLds = kBlockSize + 4 * (kFTab + 2 * kRoundPos + 2 * kWavesPerBlock) + kPW * kLevels * kRow;
 static_assert(kFastLds <= 160 * 1024, "fast compressor LDS exceeds a CU");
 
 hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s) {

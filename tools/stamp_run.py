@@ -22,8 +22,8 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 NAMES = ["ring+flush", "walk", "decode", "longlit", "in-order tail", "big literals", "", "", "round"]
-CNAMES = ["inserts", "B1 wait", "candidates", "long matches", "parse", "tokens+sizes", "prefetch",
-          "B2 wait", "layout", "emission", "tail"]
+CNAMES = ["candidates", "long matches", "parse", "tokens+sizes", "barrier wait", "layout", "emission", "tail"]
+INAMES = ["inserter: inserts", "inserter: barrier wait"]
 
 
 def main():
@@ -82,12 +82,15 @@ def compress_stamps(args):
     torch.cuda.synchronize()
     fn(buf, 1)
     v = list(buf)
-    rounds = v[11]
-    tot = sum(v[:11])
-    print("compress_fast %s: %d wave-rounds" % (args.data, rounds))
+    rounds, irounds = v[11], v[10]
+    tot = sum(v[:8])
+    print("compress_fast %s: %d parse wave-rounds, %d inserter rounds" % (args.data, rounds, irounds))
     for i, nme in enumerate(CNAMES):
-        print("  %-14s %5.1f%%  %7.0f cycles/wave-round" % (nme, 100.0 * v[i] / tot, v[i] / max(rounds, 1)))
-    print("  total          %7.0f cycles/wave-round" % (tot / max(rounds, 1)))
+        print("  %-24s %5.1f%%  %7.0f cycles/wave-round" % (nme, 100.0 * v[i] / tot, v[i] / max(rounds, 1)))
+    print("  total (parse waves)      %7.0f cycles/wave-round" % (tot / max(rounds, 1)))
+    itot = v[8] + v[9]
+    for i, nme in enumerate(INAMES):
+        print("  %-24s %5.1f%%  %7.0f cycles/round" % (nme, 100.0 * v[8 + i] / max(itot, 1), v[8 + i] / max(irounds, 1)))
 
 
 XNAMES = ["search", "literal emit", "match length", "emit+hash+table+verify", "loop top", "remainder"]
