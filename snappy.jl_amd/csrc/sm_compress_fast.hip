@@ -25,7 +25,7 @@
 #include "sm_device.h"
 #include "sm_internal.h"
 
-#ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches
+#ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches, 4 inserter only
 #define SM_ABLATE 0
 #endif
 
@@ -33,6 +33,7 @@ namespace sm {
 
 #if SM_STAMP
 __device__ unsigned long long g_stamp_c[12];
+__device__ unsigned long long g_stamp_w[16];  // barrier wait per wave index
 #endif
 STAMP_MACROS(12)
 
@@ -107,36 +108,59 @@ __device__ inline void put_copy_cf(uint8_t* dst, uint32_t o, uint32_t off, uint3
 #define SM_FAST_HASHAHEAD 0  // 1: the parse waves hash positions two rounds ahead for the inserter
 #endif
 
+// Fast-mode hash of the 4 bytes at a position: full-rate 24-bit multiply (v_mul_u32_u24) of
+// the word folded to 24 bits, bits 10..23 of the product (the reference's 32-bit multiply,
+// internal.jl:94, is quarter rate; fast mode only needs a good spread -- ratio 0.5545 against
+// 0.5538 with the reference hash in tools/fastparse_model.c terms).
+__device__ inline uint32_t fast_hash(uint32_t w) {
+  uint32_t p;  // the compiler widens a masked 24-bit product to v_mul_lo_u32: issue it directly
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(p) : "s"(0x1e35a7u), "v"(w ^ (w >> 12)));
+  return (p >> 10) & (kFTab - 1);
+}
+
 // Hash slot of position q for the inserter (0xffff: no 4 bytes at q, not inserted).
 __device__ inline uint32_t hash_slot(const uint8_t* data, uint32_t q, uint32_t n) {
-  return q + 4 <= n ? (lds_ld32(data, q) * kHashMul) >> (32 - kFTabBits) : 0xffffu;
+  return q + 4 <= n ? fast_hash(lds_ld32(data, q)) : 0xffffu;
 }
 
 // Inserter: positions [r0, r0 + kRoundPos) in order; ring[i] receives the candidates of
 // position r0 + i (the old table entry).  kG groups of 64 positions per step so the LDS round
-// trips overlap.
+// trips overlap.  r0 is a multiple of 64: the words come from aligned dwords (immediate
+// offsets), and reads past n stay inside the LDS allocation (the table follows the block).
 __device__ inline void insert_round(const uint8_t* data, uint32_t* T, uint32_t* ring, uint32_t r0, uint32_t n,
                                     uint32_t lane) {
-  constexpr int kG = 6;
+#ifndef SM_FAST_KG
+#define SM_FAST_KG 6
+#endif
+  constexpr int kG = SM_FAST_KG;
   static_assert((kRoundPos / 64) % kG == 0, "insert step");
   if (r0 >= n) return;
   const uint32_t ngroups = min((n - r0 + 63) >> 6, kRoundPos / 64);
+  const bool full = r0 + kRoundPos + 3 <= n;  // every position of the round has its 4 bytes
+  const uint32_t sh = lane & 3u;
   for (uint32_t g0 = 0; g0 < ngroups; g0 += kG) {
+    const uint32_t base = r0 + 64 * g0;
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(data + base) + (lane >> 2);
     uint32_t h[kG], old[kG];
-#pragma unroll
-    for (int i = 0; i < kG; ++i)
-      h[i] = SM_FAST_HASHAHEAD ? ring[64 * (g0 + i) + lane] & 0xffffu : hash_slot(data, r0 + 64 * (g0 + i) + lane, n);
+    bool ok[kG];
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
-      const uint32_t q = r0 + 64 * (g0 + i) + lane;
+      h[i] = fast_hash(__builtin_amdgcn_alignbyte(dw[16 * i + 1], dw[16 * i], sh));
+      ok[i] = full || SM_FAST_HASHAHEAD || base + 64 * i + lane + 4 <= n;
+      if (SM_FAST_HASHAHEAD) {
+        h[i] = ring[64 * (g0 + i) + lane] & 0xffffu;
+        ok[i] = h[i] != 0xffffu && base + 64 * i + lane + 4 <= n;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
       old[i] = 0;
-      if (h[i] != 0xffffu && q + 4 <= n) old[i] = __hip_atomic_exchange(&T[h[i]], q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (ok[i]) old[i] = __hip_atomic_exchange(&T[h[i]], base + 64 * i + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       // the old latest becomes the second-latest (the new entry's high half)
-      const uint32_t q = r0 + 64 * (g0 + i) + lane;
-      if (kDepth > 1 && h[i] != 0xffffu && q + 4 <= n) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
+      if (kDepth > 1 && ok[i]) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
       ring[64 * (g0 + i) + lane] = old[i];
     }
   }
@@ -223,7 +247,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   STAMP_DECL
   for (uint32_t r = 0; r < rounds; ++r) {
     const uint32_t k = r * kPW + wave;
-    const bool active = !inserter && k < nchunks;
+    const bool active = !inserter && k < nchunks && !(SM_ABLATE & 4);
     const uint32_t c0 = k * kChunk;
     const uint32_t ce = active ? min(c0 + kChunk, n) : c0;
     uint32_t* cinfo = csize + (r & 1) * kWavesPerBlock;
@@ -351,19 +375,20 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         }
 #endif
         // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles
+        // (length | offset << 8 packed: one shuffle per register)
         const uint32_t ci = c & 63u;
-        const uint32_t l0 = __shfl(Ls[0], ci, 64), l1 = __shfl(Ls[1], ci, 64);
-        const uint32_t o0 = __shfl(offs[0], ci, 64), o1 = __shfl(offs[1], ci, 64);
-        const uint32_t Lc = c < 64 ? l0 : (c < kChunk ? l1 : 0u);
-        const uint32_t oc = c < 64 ? o0 : o1;
+        const uint32_t v0 = __shfl(Ls[0] | (offs[0] << 8), ci, 64), v1 = __shfl(Ls[1] | (offs[1] << 8), ci, 64);
+        const uint32_t vc = c < 64 ? v0 : (c < kChunk ? v1 : 0u);
+        const uint32_t Lc = vc & 0xffu;
         const bool istok = lane < 32 && Lc != 0;
         const uint64_t tm = ballot(istok);
         nmatch = (uint32_t)__builtin_popcountll(tm);
         const uint32_t sh = (uint32_t)(tm & 1u) ^ 1u;  // tokens start at lane 1 if 0 is no match
-        const uint32_t tav = __shfl(c | (Lc << 16), lane + sh, 64), tbv = __shfl(oc, lane + sh, 64);
+        // token: position | length << 8 | offset << 16 (position < 128, length <= 128, offset < 65536)
+        const uint32_t tv = __shfl(c | (vc << 8), lane + sh, 64);
         if (nmatch) {
-          ta = tav;
-          tb = tbv;
+          ta = (tv & 0xffu) | ((tv >> 8) & 0xffu) << 16;
+          tb = tv >> 16;
           last_end = readlane(c + Lc, nmatch - 1 + sh);
         }
 #if !SM_FAST_WALK
@@ -388,7 +413,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       }
       const uint32_t tq = c0 + (ta & 0xffff), tL = ta >> 16;
       const uint32_t end = tq + tL;
-      const uint32_t prev_end = __shfl_up(end, 1, 64);
+      const uint32_t prev_end = __builtin_amdgcn_update_dpp(0u, end, 0x138, 0xf, 0xf, false);  // wave_shr:1
       ls = lane == 0 ? c0 : prev_end;
       if (lane < ntok) {
         litlen = tq - ls;
@@ -428,31 +453,35 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     //               and its tag encodes the run length up to the end of the last piece.
     uint32_t myb, mycont, myrun, total;
     {
+      static_assert(kPW < 16, "the round layout runs in DPP row 0");
       const uint32_t info = lane < kPW ? cinfo[lane] : 0u;
       const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0xffu, trl = (info >> 19) & 0xffu;
       const bool nocp = (info >> 27) & 1u;
-      const uint32_t trl_prev = __shfl_up(trl, 1, 64);
+      const uint32_t trl_prev = __builtin_amdgcn_update_dpp(0u, trl, 0x111, 0xf, 0xf, true);  // row_shr:1
       const bool cont_in = lane > 0 && lane < kPW && trl_prev > 0 && lead > 0;
       const bool mid = nocp && cont_in;
       const bool start = trl > 0 && !mid;
-      const bool cont_next = __shfl_down((uint32_t)cont_in, 1, 64) != 0 && lane + 1 < kPW;
+      const bool cont_next = __builtin_amdgcn_update_dpp(0u, (uint32_t)cont_in, 0x101, 0xf, 0xf, true) != 0;  // row_shl:1
       const uint32_t cu = (r * kPW + lane) * kChunk;                         // chunk start
       const uint32_t ceu = min(cu + kChunk, n);
       // the run ending in chunk u ends at cu + lead; a run starting in chunk v ends in the
       // first later chunk whose piece ends it (suffix min over lanes)
       const bool ends = cont_in && !(mid && cont_next);
       uint32_t nxt = ends ? lane : 0xffu;
-#pragma unroll
-      for (uint32_t d = 1; d < kWavesPerBlock; d <<= 1) {
-        const uint32_t o2 = __shfl_down(nxt, d, 64);
-        nxt = (lane + d < kPW && o2 < nxt) ? o2 : nxt;
-      }
-      nxt = __shfl_down(nxt, 1, 64);                                         // first end after u
+      nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x101, 0xf, 0xf, false));  // row_shl:1
+      nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x102, 0xf, 0xf, false));  // row_shl:2
+      nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x104, 0xf, 0xf, false));  // row_shl:4
+      nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x108, 0xf, 0xf, false));  // row_shl:8
+      nxt = __builtin_amdgcn_update_dpp(0xffu, nxt, 0x101, 0xf, 0xf, false);                       // first end after u
       const uint32_t endpos = __shfl(cu + lead, nxt & 63u, 64);
       const uint32_t runlen = (start && cont_next) ? endpos - (ceu - trl) : 0u;
       const uint32_t Sm = S - (cont_in ? lit_tag_bytes(lead) : 0u) +
                           (runlen ? lit_tag_bytes(runlen) - lit_tag_bytes(trl) : 0u);
-      const uint32_t inclm = scan_dpp(lane < kPW ? Sm : 0u);
+      uint32_t inclm = lane < kPW ? Sm : 0u;
+      inclm += __builtin_amdgcn_update_dpp(0u, inclm, 0x111, 0xf, 0xf, true);  // row_shr:1
+      inclm += __builtin_amdgcn_update_dpp(0u, inclm, 0x112, 0xf, 0xf, true);  // row_shr:2
+      inclm += __builtin_amdgcn_update_dpp(0u, inclm, 0x114, 0xf, 0xf, true);  // row_shr:4
+      inclm += __builtin_amdgcn_update_dpp(0u, inclm, 0x118, 0xf, 0xf, true);  // row_shr:8
       total = readlane(inclm, kPW - 1);
       myb = readlane(inclm - Sm, wave);
       mycont = readlane((uint32_t)cont_in, wave);
@@ -494,15 +523,20 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   }
   STAMP(7)
   STAMP_FLUSH(g_stamp_c)
+#if SM_STAMP
+  if (lane == 0) atomicAdd(&g_stamp_w[wave], (unsigned long long)(inserter ? st_acc[9] : st_acc[4]));
+#endif
   if (tid == 0) a.out_len[b] = op;
 }
 
 #if SM_STAMP
 extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_c), sizeof(g_stamp_c)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out + 12, HIP_SYMBOL(g_stamp_w), sizeof(g_stamp_w)) != hipSuccess) return -1;
   if (reset) {
-    unsigned long long z[12] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_c), z, sizeof(z)) != hipSuccess) return -1;
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_c), z, sizeof(g_stamp_c)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_w), z, sizeof(g_stamp_w)) != hipSuccess) return -1;
   }
   return 0;
 }

@@ -75,7 +75,7 @@ def compress_stamps(args):
     b = bench.Batch(blocks, dev)
     b.compress(sm, "fast")
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * 12)()
+    buf = (ctypes.c_ulonglong * 28)()
     fn(buf, 1)
     for _ in range(args.reps):
         b.compress(sm, "fast")
@@ -91,6 +91,8 @@ def compress_stamps(args):
     itot = v[8] + v[9]
     for i, nme in enumerate(INAMES):
         print("  %-24s %5.1f%%  %7.0f cycles/round" % (nme, 100.0 * v[8 + i] / max(itot, 1), v[8 + i] / max(irounds, 1)))
+    print("  barrier wait per wave index (cycles/round): " +
+          " ".join("%d" % (v[12 + w] / max(irounds, 1)) for w in range(16)))
 
 
 XNAMES = ["search", "literal emit", "match length", "emit+hash+table+verify", "loop top", "remainder"]
