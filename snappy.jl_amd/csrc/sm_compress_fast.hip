@@ -6,21 +6,21 @@
 //
 // One workgroup of 16 waves per block, in two roles:
 //  * the INSERTER (wave 15) walks the block's positions in order, 64 per instruction, through
-//    a 16 K-entry hash table with ds_wrxchg_rtn_b32.  A wave's LDS instructions execute in
-//    order and the conflicting lanes of one instruction in ascending lane order, so the value
-//    each position gets back is exactly the sequential one: the latest and the second-latest
-//    earlier position with the same hash (a table entry holds both: the exchange puts the new
-//    position in the low half and a ds_write_b16 moves the old latest into the high half).
-//    Correctness never depends on that order -- every candidate is verified -- only the ratio
-//    does.  The candidates go to a per-round LDS ring, one round ahead of the parse.
-//  * 15 PARSE waves.  The block is cut into 128-byte chunks whose parse never crosses the chunk
-//    end (copies are truncated there, literal runs end there), so the chunks of a round are
-//    parsed independently: in round r parse wave w owns chunk 15r+w, two positions per lane.
-//    Per chunk: verify and extend the 1-2 chain candidates of every position, greedy parse by
-//    pointer doubling (J_k = J_{k-1} o J_{k-1}), token sizes in closed form and a DPP scan,
-//    then (after the round barrier) the round layout over the 15 chunks -- literal runs that
-//    cross chunk boundaries are merged -- and the emission: token lanes write tag bytes,
-//    position lanes scatter literal bytes.
+//    a hash table with ds_wrxchg_rtn_b32.  A wave's LDS instructions execute in order and the
+//    conflicting lanes of one instruction in ascending lane order, so the value each position
+//    gets back is exactly the sequential one: the latest and the second-latest earlier
+//    position with the same hash (a table entry holds both: the exchange puts the new position
+//    in the low half and a ds_write_b16 moves the old latest into the high half).  Correctness
+//    never depends on that order -- every candidate is verified -- only the ratio does.  The
+//    candidates go to a per-round LDS ring, one round ahead of the parse.
+//  * 15 PARSE waves.  The block is cut into kChunk-byte chunks whose parse never crosses the
+//    chunk end (copies are truncated there, literal runs end there), so the chunks of a round
+//    are parsed independently: in round r parse wave w owns chunk 15r+w, kChunk/64 positions
+//    per lane (q = c0 + 64j + lane).  Per chunk: verify and extend the chain candidates of
+//    every position, greedy parse by pointer doubling (J_k = J_{k-1} o J_{k-1}), token sizes
+//    in closed form and a DPP scan, then (after the round barrier) the round layout over the 15
+//    chunks -- literal runs that cross chunk boundaries are merged -- and the emission: token
+//    lanes write tag bytes, position lanes scatter literal bytes.
 // One barrier per round (chunk infos are double-buffered).  Output is deterministic.
 #include "sm_device.h"
 #include "sm_internal.h"
@@ -37,22 +37,31 @@ __device__ unsigned long long g_stamp_w[16];  // barrier wait per wave index
 #endif
 STAMP_MACROS(12)
 
-constexpr uint32_t kFTabBits = 14;
-constexpr uint32_t kFTab = 1u << kFTabBits;   // hash table entries: u32 = (second-latest+1) << 16 | (latest+1)
-constexpr uint32_t kChunk = 128;
+#ifndef SM_FAST_CHUNK
+#define SM_FAST_CHUNK 256
+#endif
+constexpr uint32_t kChunk = SM_FAST_CHUNK;     // bytes per chunk: 128 or 256
+static_assert(kChunk == 128 || kChunk == 256, "chunk size");
+constexpr int kP = kChunk / 64;                // positions per lane
+// hash table entries, u32 = (second-latest+1) << 16 | (latest+1); 256-byte chunks need the
+// LDS for their ring and jump tables, so their table is 8 K entries
+constexpr uint32_t kFTabBits = kChunk == 256 ? 13 : 14;
+constexpr uint32_t kFTab = 1u << kFTabBits;
 constexpr uint32_t kWavesPerBlock = 16;
 constexpr uint32_t kPW = kWavesPerBlock - 1;  // parse waves; wave kPW is the inserter
 constexpr uint32_t kThreads = 64 * kWavesPerBlock;
-constexpr uint32_t kRoundPos = kPW * kChunk;  // positions per round (1920)
-constexpr uint32_t kLevels = 5;               // J0..J4: the copy-to-copy walk of a chunk takes <= 31 steps
-constexpr uint32_t kRow = kChunk + 8;         // a jump-table row (8-B aligned); entry kChunk, the chunk end, is its own image
+constexpr uint32_t kRoundPos = kPW * kChunk;  // positions per round
+// J0..J_{kLevels-1}: a chunk holds <= kChunk/4 copies, so its walk takes < kChunk/4 steps
+constexpr uint32_t kLevels = kChunk == 256 ? 6 : 5;
+// the chain's end marker: the chunk end (128 fits a byte); for 256-byte chunks position 255,
+// which is never a match (a match needs 4 bytes), so "the first match at or after x" never
+// names it and it maps to itself at every level
+constexpr uint32_t kEnd = kChunk == 256 ? 255 : kChunk;
+constexpr uint32_t kRow = kChunk + 8;         // a jump-table row (8-B aligned)
 #ifndef SM_FAST_DEPTH
 #define SM_FAST_DEPTH 2
 #endif
-constexpr int kDepth = SM_FAST_DEPTH;
-#ifndef SM_FAST_WALK
-#define SM_FAST_WALK 0                        // 1: scalar walk of the parse chain; 0: pointer doubling in LDS
-#endif         // chain candidates verified per position (1: latest, 2: + second-latest)
+constexpr int kDepth = SM_FAST_DEPTH;         // chain candidates verified per position (1: latest, 2: + second-latest)
 
 // literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
 __device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
@@ -77,10 +86,11 @@ __device__ inline uint32_t copy_bytes_cf(uint32_t off, uint32_t L) {
   return 3 * (k + e) + ((R < 12 && off < 2048) ? 2 : 3);
 }
 
-// emit_copy! bytes (internal.jl:289-329) for L <= 128 (at most one 64-piece)
+// emit_copy! bytes (internal.jl:289-329): 64-byte pieces while L >= 68, a 60 if L > 64, then
+// the rest as copy-1 (L < 12, off < 2048) or copy-2
 __device__ inline void put_copy_cf(uint8_t* dst, uint32_t o, uint32_t off, uint32_t L) {
   const uint8_t lo = (uint8_t)off, hi = (uint8_t)(off >> 8);
-  if (L >= 68) {
+  while (L >= 68) {
     dst[o] = (uint8_t)(2 + (63 << 2));
     dst[o + 1] = lo;
     dst[o + 2] = hi;
@@ -104,23 +114,18 @@ __device__ inline void put_copy_cf(uint8_t* dst, uint32_t o, uint32_t off, uint3
   }
 }
 
-#ifndef SM_FAST_HASHAHEAD
-#define SM_FAST_HASHAHEAD 0  // 1: the parse waves hash positions two rounds ahead for the inserter
+#ifndef SM_FAST_PRIO
+#define SM_FAST_PRIO 3
 #endif
 
 // Fast-mode hash of the 4 bytes at a position: full-rate 24-bit multiply (v_mul_u32_u24) of
-// the word folded to 24 bits, bits 10..23 of the product (the reference's 32-bit multiply,
+// the word folded to 24 bits, bits 10.. of the product (the reference's 32-bit multiply,
 // internal.jl:94, is quarter rate; fast mode only needs a good spread -- ratio 0.5545 against
 // 0.5538 with the reference hash in tools/fastparse_model.c terms).
 __device__ inline uint32_t fast_hash(uint32_t w) {
   uint32_t p;  // the compiler widens a masked 24-bit product to v_mul_lo_u32: issue it directly
   asm("v_mul_u32_u24 %0, %1, %2" : "=v"(p) : "s"(0x1e35a7u), "v"(w ^ (w >> 12)));
   return (p >> 10) & (kFTab - 1);
-}
-
-// Hash slot of position q for the inserter (0xffff: no 4 bytes at q, not inserted).
-__device__ inline uint32_t hash_slot(const uint8_t* data, uint32_t q, uint32_t n) {
-  return q + 4 <= n ? fast_hash(lds_ld32(data, q)) : 0xffffu;
 }
 
 // Inserter: positions [r0, r0 + kRoundPos) in order; ring[i] receives the candidates of
@@ -146,11 +151,7 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, uint32_t* 
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       h[i] = fast_hash(__builtin_amdgcn_alignbyte(dw[16 * i + 1], dw[16 * i], sh));
-      ok[i] = full || SM_FAST_HASHAHEAD || base + 64 * i + lane + 4 <= n;
-      if (SM_FAST_HASHAHEAD) {
-        h[i] = ring[64 * (g0 + i) + lane] & 0xffffu;
-        ok[i] = h[i] != 0xffffu && base + 64 * i + lane + 4 <= n;
-      }
+      ok[i] = full || base + 64 * i + lane + 4 <= n;
     }
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
@@ -211,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     uint4* t16 = reinterpret_cast<uint4*>(T);
     for (uint32_t k = tid; k < kFTab / 4; k += kThreads) t16[k] = z;  // 0 = no position
   }
-  if (!inserter && lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
+  if (!inserter && kEnd == kChunk && lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
   uint32_t op = 0;
   if (a.header) {
     uint32_t nb = varint_len(n);
@@ -222,23 +223,15 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
 
   const uint32_t nchunks = (n + kChunk - 1) / kChunk;
   const uint32_t rounds = (nchunks + kPW - 1) / kPW;
-#ifndef SM_FAST_PRIO
-#define SM_FAST_PRIO 3
-#endif
   // the inserter shares a SIMD with three parse waves and gates every round: issue it first
   if (inserter && SM_FAST_PRIO) __builtin_amdgcn_s_setprio(SM_FAST_PRIO);
-  // hash slots of rounds 0 and 1 (later rounds: two rounds ahead, by the parse waves)
-  if (SM_FAST_HASHAHEAD) {
-    for (uint32_t i = tid; i < 2 * kRoundPos; i += kThreads) ring[i] = hash_slot(data, i, n);
-    __syncthreads();
-  }
   if (inserter) insert_round(data, T, ring, 0, n, lane);
   __syncthreads();
 
-  uint64_t w[2];  // the 8 bytes at each position
+  uint64_t w[kP];  // the 8 bytes at each position
   if (!inserter) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < kP; ++j) {
       uint32_t q = wave * kChunk + 64 * j + lane;
       w[j] = lds_ld64(data, q < n ? q : 0);
     }
@@ -252,7 +245,9 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     const uint32_t ce = active ? min(c0 + kChunk, n) : c0;
     uint32_t* cinfo = csize + (r & 1) * kWavesPerBlock;
     uint32_t ta = 0, tb = 0, ntok = 0, incl = 0, sz = 0, litlen = 0, littag = 0, ls = 0;
-    uint64_t ts0 = 0, ts1 = 0, wn[2] = {0, 0};
+    uint64_t ts[kP], wn[kP];
+#pragma unroll
+    for (int j = 0; j < kP; ++j) ts[j] = wn[j] = 0;
 
     if (inserter) {
       insert_round(data, T, ring + ((r + 1) & 1) * kRoundPos, (r + 1) * kRoundPos, n, lane);
@@ -262,10 +257,10 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       STAMP_COUNT(11, 1)
       // (a) candidates: the latest (and second-latest) earlier position with the same hash,
       // verified and extended 8 bytes at a time; the longest wins (ties: the latest).
-      uint32_t* cr = ring + (r & 1) * kRoundPos + wave * kChunk;
-      uint32_t Ls[2], offs[2];
+      const uint32_t* cr = ring + (r & 1) * kRoundPos + wave * kChunk;
+      uint32_t Ls[kP], offs[kP];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < kP; ++j) {
         const uint32_t q = c0 + 64 * j + lane;
         const bool can = q + 4 <= ce;
         const uint32_t cv = cr[64 * j + lane];
@@ -285,15 +280,10 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         Ls[j] = min(L, ce - q);
         offs[j] = q - c;
       }
-      // this slot's next use: the hash slots of the same chunk index two rounds ahead
-      if (SM_FAST_HASHAHEAD) {
-#pragma unroll
-        for (int j = 0; j < 2; ++j) cr[64 * j + lane] = hash_slot(data, c0 + 2 * kRoundPos + 64 * j + lane, n);
-      }
       STAMP(0)
       // finish matches that filled the 8-byte window: 8 bytes per lane per step
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < kP; ++j) {
         const uint32_t q = c0 + 64 * j + lane;
         uint32_t L = Ls[j];
         bool more = L >= 8 && q + L < ce;
@@ -309,99 +299,90 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         Ls[j] = (SM_ABLATE & 2) ? 0u : L;
       }
       STAMP(1)
-      // Greedy parse by pointer doubling (no serial loop) over the chunk's 128 positions.
-      // J0 skips literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a
-      // non-match), else the chunk end, so the greedy walk from 0 steps only between copies
-      // (<= 32 copies of >= 4 bytes: 31 steps); J_k = J_{k-1} o J_{k-1}, k < 5.  Copy t of the
-      // chunk is then computed directly in lane t from the jump tables.
-      // no copies at all (incompressible): skip the parse
-      const uint64_t M0 = ballot(Ls[0] != 0), M1 = ballot(Ls[1] != 0);
-      uint32_t nmatch = 0, last_end = 0;
-      if (M0 | M1) {
-        uint32_t jv[2];
+      // Greedy parse by pointer doubling (no serial loop) over the chunk's positions.  J0
+      // skips literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a
+      // non-match), else kEnd, so the greedy walk from 0 steps only between copies;
+      // J_k = J_{k-1} o J_{k-1}.  Chain element t of the chunk is then computed directly in
+      // lane t from the jump tables.  No copies at all (incompressible): no parse.
+      uint64_t M[kP];
+      uint64_t any = 0;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < kP; ++j) {
+        M[j] = ballot(Ls[j] != 0);
+        any |= M[j];
+      }
+      uint32_t nmatch = 0, last_end = 0;
+      if (any) {
+        // F[i]: the first match position in words > i (kEnd: none)
+        uint32_t F[kP];
+        F[kP - 1] = kEnd;
+#pragma unroll
+        for (int i = kP - 2; i >= 0; --i) F[i] = M[i + 1] ? 64u * (i + 1) + ctz64(M[i + 1]) : F[i + 1];
+        uint32_t jv[kP];
+#pragma unroll
+        for (int j = 0; j < kP; ++j) {
           const uint32_t rr = 64 * j + lane;
-          const uint32_t x = rr + Ls[j];  // <= 128: copies end inside the chunk
-          const uint64_t m0 = x < 64 ? M0 >> x : 0;
-          const uint64_t m1 = x < 64 ? M1 : (x < 128 ? M1 >> (x - 64) : 0);
-          const uint32_t b1 = x < 64 ? 64u : x;
-          jv[j] = m0 ? x + (uint32_t)__builtin_ctzll(m0) : (m1 ? b1 + (uint32_t)__builtin_ctzll(m1) : kChunk);
-#if !SM_FAST_WALK
+          const uint32_t x = rr + Ls[j];  // <= kChunk: copies end inside the chunk
+          const uint32_t i = x >> 6;
+          uint64_t mw = M[0];
+#pragma unroll
+          for (int t = 1; t < kP; ++t) mw = i == (uint32_t)t ? M[t] : mw;
+          uint32_t f = kEnd;
+#pragma unroll
+          for (int t = 0; t < kP; ++t) f = i == (uint32_t)t ? F[t] : f;
+          const uint64_t m = i < (uint32_t)kP ? mw >> (x & 63u) : 0;
+          jv[j] = m ? x + ctz64(m) : f;
           jt[rr] = (uint8_t)jv[j];
-#endif
         }
-#if SM_FAST_WALK
-        // chain element t (lane t) by a scalar walk: position 0, then J0 of the previous
-        // element; the copy-start bitmask is built on the way.  Steps = copies + 1.
-        uint32_t c = kChunk;
-        {
-          uint32_t p = 0, t = 0;
-          uint64_t s0 = 0, s1 = 0;
-          while (p < kChunk) {
-            c = lane == t ? p : c;
-            const uint32_t l = p & 63u;
-            const bool hi = p >= 64;
-            const bool ism = ((hi ? M1 : M0) >> l) & 1u;
-            if (ism) {
-              if (hi) s1 |= 1ull << l;
-              else s0 |= 1ull << l;
-            }
-            const uint32_t a0 = readlane(jv[0], l), a1 = readlane(jv[1], l);
-            p = hi ? a1 : a0;
-            ++t;
-          }
-          ts0 = s0;
-          ts1 = s1;
-        }
-#else
 #pragma unroll
         for (int kk = 1; kk < (int)kLevels; ++kk) {
           __atomic_signal_fence(__ATOMIC_SEQ_CST);
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < kP; ++j) {
             jv[j] = jt[(kk - 1) * kRow + jv[j]];
             jt[kk * kRow + 64 * j + lane] = (uint8_t)jv[j];
           }
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        // chain element t (lane t < 32) from position 0: J_k for every set bit k of t.  Only
-        // element 0 can be a non-match (J0 jumps to match positions), the rest are the copies.
+        // chain element t (lane t < kChunk/4) from position 0: J_k for every set bit k of t.
+        // Only element 0 can be a non-match (J0 jumps to match positions), the rest are the
+        // copies; past the last copy the chain sits at kEnd (no match).
         uint32_t c = 0;
 #pragma unroll
         for (int kk = 0; kk < (int)kLevels; ++kk) {
           const uint32_t t = jt[kk * kRow + c];
           c = ((lane >> kk) & 1u) ? t : c;
         }
-#endif
-        // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles
-        // (length | offset << 8 packed: one shuffle per register)
-        const uint32_t ci = c & 63u;
-        const uint32_t v0 = __shfl(Ls[0] | (offs[0] << 8), ci, 64), v1 = __shfl(Ls[1] | (offs[1] << 8), ci, 64);
-        const uint32_t vc = c < 64 ? v0 : (c < kChunk ? v1 : 0u);
-        const uint32_t Lc = vc & 0xffu;
-        const bool istok = lane < 32 && Lc != 0;
+        // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles of
+        // length | offset << 9
+        const uint32_t ci = c & 63u, cj = c >> 6;
+        uint32_t vc = 0;
+#pragma unroll
+        for (int j = 0; j < kP; ++j) {
+          const uint32_t v = __shfl(Ls[j] | (offs[j] << 9), ci, 64);
+          vc = cj == (uint32_t)j ? v : vc;
+        }
+        const uint32_t Lc = c < kEnd ? vc & 0x1ffu : 0u;
+        const bool istok = lane < kChunk / 4 && Lc != 0;
         const uint64_t tm = ballot(istok);
         nmatch = (uint32_t)__builtin_popcountll(tm);
         const uint32_t sh = (uint32_t)(tm & 1u) ^ 1u;  // tokens start at lane 1 if 0 is no match
-        // token: position | length << 8 | offset << 16 (position < 128, length <= 128, offset < 65536)
-        const uint32_t tv = __shfl(c | (vc << 8), lane + sh, 64);
+        // token: position | length << 16; offset
+        const uint32_t tav = __shfl(c | (Lc << 16), lane + sh, 64), tbv = __shfl(vc >> 9, lane + sh, 64);
         if (nmatch) {
-          ta = (tv & 0xffu) | ((tv >> 8) & 0xffu) << 16;
-          tb = tv >> 16;
+          ta = tav;
+          tb = tbv;
           last_end = readlane(c + Lc, nmatch - 1 + sh);
         }
-#if !SM_FAST_WALK
         // copy-start bitmask (position p of the chunk) for the literal scatter
         uint64_t* tsw = reinterpret_cast<uint64_t*>(jt);
-        if (lane == 0) tsw[0] = tsw[1] = 0;
+        if (lane < kP) tsw[lane] = 0;
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (istok)
           __hip_atomic_fetch_or(&tsw[c >> 6], 1ull << (c & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        ts0 = tsw[0];
-        ts1 = tsw[1];
-#endif
+#pragma unroll
+        for (int j = 0; j < kP; ++j) ts[j] = tsw[j];
       }
       STAMP(2)
       ntok = nmatch;
@@ -421,15 +402,15 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         sz = littag + litlen + (tL ? copy_bytes_cf(tb, tL) : 0);
       }
       incl = scan_dpp(sz);
-      // chunk info for the round layout: unmerged size | leading literal piece | trailing
-      // literal piece | no copies at all
+      // chunk info for the round layout: unmerged size | leading literal piece << 11 |
+      // trailing literal piece << 20 | no copies at all << 29
       const uint32_t trail = ce - c0 - last_end;
       if (lane == 0)
-        cinfo[wave] = readlane(incl, ntok - 1) | (readlane(litlen, 0) << 11) | (trail << 19) | ((nmatch == 0) << 27);
+        cinfo[wave] = readlane(incl, ntok - 1) | (readlane(litlen, 0) << 11) | (trail << 20) | ((nmatch == 0) << 29);
       // next round's words
       const uint32_t c2 = (k + kPW) * kChunk;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < kP; ++j) {
         const uint32_t q = c2 + 64 * j + lane;
         wn[j] = lds_ld64(data, q < n ? q : 0);
       }
@@ -455,8 +436,8 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     {
       static_assert(kPW < 16, "the round layout runs in DPP row 0");
       const uint32_t info = lane < kPW ? cinfo[lane] : 0u;
-      const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0xffu, trl = (info >> 19) & 0xffu;
-      const bool nocp = (info >> 27) & 1u;
+      const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0x1ffu, trl = (info >> 20) & 0x1ffu;
+      const bool nocp = (info >> 29) & 1u;
       const uint32_t trl_prev = __builtin_amdgcn_update_dpp(0u, trl, 0x111, 0xf, 0xf, true);  // row_shr:1
       const bool cont_in = lane > 0 && lane < kPW && trl_prev > 0 && lead > 0;
       const bool mid = nocp && cont_in;
@@ -505,21 +486,20 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       const uint32_t end = tq + tL;
       uint32_t below = 0;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const uint64_t ts = j == 0 ? ts0 : ts1;
+      for (int j = 0; j < kP; ++j) {
         const uint32_t x = c0 + 64 * j + lane;
-        uint32_t cnt = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(ts >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ts, 0u));
-        cnt += (uint32_t)(ts >> lane) & 1u;  // tokens whose copy starts at or before x
+        uint32_t cnt = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(ts[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ts[j], 0u));
+        cnt += (uint32_t)(ts[j] >> lane) & 1u;  // tokens whose copy starts at or before x
         const uint32_t pend = __shfl(end, cnt ? cnt - 1 : 0, 64);
         const int32_t dl = __shfl(delta, cnt, 64);
         if (x < ce && (cnt == 0 || x >= pend)) dst[(int32_t)x + dl] = (uint8_t)w[j];
-        below += __builtin_popcountll(ts);
+        below += __builtin_popcountll(ts[j]);
       }
     }
     STAMP(6)
     op += total;
-    w[0] = wn[0];
-    w[1] = wn[1];
+#pragma unroll
+    for (int j = 0; j < kP; ++j) w[j] = wn[j];
   }
   STAMP(7)
   STAMP_FLUSH(g_stamp_c)
