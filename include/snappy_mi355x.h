@@ -12,10 +12,12 @@
  * code (16..21), sm_status_message() returns the reference's exact text, and codes 1/2 keep
  * libsnappy's meaning (INVALID_INPUT, BUFFER_TOO_SMALL).
  *
- * Two compress modes:
- *   SM_MODE_REFERENCE -- output byte-identical to Snappy.jl compress() (incl. its quirks);
- *   SM_MODE_FAST      -- wave-parallel parse; any output decodes bit-exactly under
- *                        Snappy.jl uncompress() and libsnappy, bytes differ from the reference.
+ * Three compress modes:
+ *   SM_MODE_REFERENCE  -- output byte-identical to Snappy.jl compress() (incl. its quirks);
+ *   SM_MODE_FAST       -- wave-parallel parse; any output decodes bit-exactly under
+ *                         Snappy.jl uncompress() and libsnappy, bytes differ from the reference;
+ *   SM_MODE_FAST_DENSE -- SM_MODE_FAST verifying two hash-chain candidates per position:
+ *                         smaller output, about 10% slower.
  * Decompression has one mode, with the reference's accept/reject behaviour.
  *
  * Threading: an sm_ctx owns one HIP device, one stream and its scratch; calls on one ctx
@@ -46,7 +48,7 @@ enum {
   SM_ERR_ARGUMENT = 33         /* bad argument (NULL, block > 64 KiB in a batch, ...) */
 };
 
-enum { SM_MODE_REFERENCE = 0, SM_MODE_FAST = 1 };
+enum { SM_MODE_REFERENCE = 0, SM_MODE_FAST = 1, SM_MODE_FAST_DENSE = 2 };
 
 #define SM_BLOCK_SIZE 65536u /* src/internal.jl:31 K_BLOCK_SIZE */
 

@@ -32,7 +32,7 @@ BLOCK_SIZE = 65536
 
 SM_OK = 0
 SM_BUFFER_TOO_SMALL = 2
-MODES = {"reference": 0, "fast": 1}
+MODES = {"reference": 0, "fast": 1, "dense": 2}
 
 # exported symbols of include/snappy_mi355x.h (checked by tests/test_abi.py)
 ABI_SYMBOLS = (
@@ -141,7 +141,7 @@ def context(device=0):
 
 def _mode(mode):
     if mode not in MODES:
-        raise ValueError("mode must be 'reference' or 'fast'")
+        raise ValueError("mode must be 'reference', 'fast' or 'dense'")
     return MODES[mode]
 
 

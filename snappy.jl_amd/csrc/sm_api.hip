@@ -47,6 +47,8 @@ struct sm_ctx {
 
 namespace {
 
+bool valid_mode(int m) { return m == SM_MODE_REFERENCE || m == SM_MODE_FAST || m == SM_MODE_FAST_DENSE; }
+
 struct DeviceGuard {
   int prev = -1;
   explicit DeviceGuard(int dev) {
@@ -290,7 +292,7 @@ void* sm_ctx_stream(sm_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
                                    const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                    const uint64_t* d_out_off, uint32_t* d_out_len, int mode, void* stream) {
-  if (!ctx || (mode != SM_MODE_REFERENCE && mode != SM_MODE_FAST)) return SM_ERR_ARGUMENT;
+  if (!ctx || !valid_mode(mode)) return SM_ERR_ARGUMENT;
   if (nblk == 0) return SM_OK;
   if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return SM_ERR_ARGUMENT;
   DeviceGuard g(ctx->device);
@@ -303,7 +305,7 @@ sm_status sm_compress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const u
                                        const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                        const uint64_t* d_out_off, uint32_t* d_out_len, uint64_t total_len,
                                        int mode, void* stream) {
-  if (!ctx || (mode != SM_MODE_REFERENCE && mode != SM_MODE_FAST)) return SM_ERR_ARGUMENT;
+  if (!ctx || !valid_mode(mode)) return SM_ERR_ARGUMENT;
   if (total_len > 0xffffffffull) return SM_ERR_INPUT_TOO_LARGE;        // src/Snappy.jl:21
   if (nblk == 0) return SM_OK;
   if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return SM_ERR_ARGUMENT;
@@ -329,7 +331,7 @@ sm_status sm_uncompress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uin
 
 sm_status sm_compress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                             uint32_t nblk, uint8_t* out, const uint64_t* out_off, uint32_t* out_len, int mode) {
-  if (!ctx) return SM_ERR_ARGUMENT;
+  if (!ctx || !valid_mode(mode)) return SM_ERR_ARGUMENT;
   if (nblk == 0) return SM_OK;
   if (!in || !in_off || !in_len || !out || !out_off || !out_len) return SM_ERR_ARGUMENT;
   size_t in_total = 0, out_total = 0;
@@ -463,7 +465,7 @@ sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, siz
 sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed, size_t* compressed_length,
                       int mode) {
   if (!ctx || !compressed_length || (n && !input) || !compressed) return SM_ERR_ARGUMENT;
-  if (mode != SM_MODE_REFERENCE && mode != SM_MODE_FAST) return SM_ERR_ARGUMENT;
+  if (!valid_mode(mode)) return SM_ERR_ARGUMENT;
   if (n > 0xffffffffull) return SM_ERR_INPUT_TOO_LARGE;                  // Snappy.jl:21
   if (*compressed_length < sm_max_compressed_length(n)) return SM_BUFFER_TOO_SMALL;
   uint8_t hdr[5];

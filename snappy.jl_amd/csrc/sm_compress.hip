@@ -227,7 +227,7 @@ extern "C" int sm_debug_stamps_x(unsigned long long* out, int reset) {
 
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s) {
   if (a.nblk == 0) return hipSuccess;
-  if (mode != 0) return launch_compress_fast(a, s);
+  if (mode != 0) return launch_compress_fast(a, mode, s);
   hipLaunchKernelGGL(k_compress_exact, dim3(a.nblk), dim3(64), 0, s, a);
   return hipGetLastError();
 }

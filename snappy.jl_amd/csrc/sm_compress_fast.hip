@@ -43,10 +43,13 @@ STAMP_MACROS(12)
 constexpr uint32_t kChunk = SM_FAST_CHUNK;     // bytes per chunk: 128 or 256
 static_assert(kChunk == 128 || kChunk == 256, "chunk size");
 constexpr int kP = kChunk / 64;                // positions per lane
-// hash table entries, u32 = (second-latest+1) << 16 | (latest+1); 256-byte chunks need the
-// LDS for their ring and jump tables, so their table is 8 K entries
-constexpr uint32_t kFTabBits = kChunk == 256 ? 13 : 14;
-constexpr uint32_t kFTab = 1u << kFTabBits;
+// Hash table: 8 K u32 buckets, 32 KiB (the ring and the jump tables of 256-byte chunks need
+// the rest of the LDS); a bucket holds (second-latest+1) << 16 | (latest+1), the high half
+// only in depth 2 (SM_MODE_FAST_DENSE).  A 16 K-bucket u16 table updated with
+// ds_mskor_rtn_b32 (masked exchange of one half) fits the same 32 KiB: depth 1 then gives
+// ratio 0.578 instead of 0.598 on the bench text but runs 7% slower (more copies to parse).
+constexpr uint32_t kTabBits = 13;
+constexpr uint32_t kTabBytes = 4u << kTabBits;
 constexpr uint32_t kWavesPerBlock = 16;
 constexpr uint32_t kPW = kWavesPerBlock - 1;  // parse waves; wave kPW is the inserter
 constexpr uint32_t kThreads = 64 * kWavesPerBlock;
@@ -58,10 +61,6 @@ constexpr uint32_t kLevels = kChunk == 256 ? 6 : 5;
 // names it and it maps to itself at every level
 constexpr uint32_t kEnd = kChunk == 256 ? 255 : kChunk;
 constexpr uint32_t kRow = kChunk + 8;         // a jump-table row (8-B aligned)
-#ifndef SM_FAST_DEPTH
-#define SM_FAST_DEPTH 2
-#endif
-constexpr int kDepth = SM_FAST_DEPTH;         // chain candidates verified per position (1: latest, 2: + second-latest)
 
 // literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
 __device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
@@ -122,16 +121,18 @@ __device__ inline void put_copy_cf(uint8_t* dst, uint32_t o, uint32_t off, uint3
 // the word folded to 24 bits, bits 10.. of the product (the reference's 32-bit multiply,
 // internal.jl:94, is quarter rate; fast mode only needs a good spread -- ratio 0.5545 against
 // 0.5538 with the reference hash in tools/fastparse_model.c terms).
+template <uint32_t kBits>
 __device__ inline uint32_t fast_hash(uint32_t w) {
   uint32_t p;  // the compiler widens a masked 24-bit product to v_mul_lo_u32: issue it directly
   asm("v_mul_u32_u24 %0, %1, %2" : "=v"(p) : "s"(0x1e35a7u), "v"(w ^ (w >> 12)));
-  return (p >> 10) & (kFTab - 1);
+  return (p >> 10) & ((1u << kBits) - 1);
 }
 
 // Inserter: positions [r0, r0 + kRoundPos) in order; ring[i] receives the candidates of
 // position r0 + i (the old table entry).  kG groups of 64 positions per step so the LDS round
 // trips overlap.  r0 is a multiple of 64: the words come from aligned dwords (immediate
 // offsets), and reads past n stay inside the LDS allocation (the table follows the block).
+template <int D>
 __device__ inline void insert_round(const uint8_t* data, uint32_t* T, uint32_t* ring, uint32_t r0, uint32_t n,
                                     uint32_t lane) {
 #ifndef SM_FAST_KG
@@ -150,7 +151,7 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, uint32_t* 
     bool ok[kG];
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
-      h[i] = fast_hash(__builtin_amdgcn_alignbyte(dw[16 * i + 1], dw[16 * i], sh));
+      h[i] = fast_hash<kTabBits>(__builtin_amdgcn_alignbyte(dw[16 * i + 1], dw[16 * i], sh));
       ok[i] = full || base + 64 * i + lane + 4 <= n;
     }
 #pragma unroll
@@ -161,17 +162,18 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, uint32_t* 
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       // the old latest becomes the second-latest (the new entry's high half)
-      if (kDepth > 1 && ok[i]) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
-      ring[64 * (g0 + i) + lane] = old[i];
+      if (D > 1 && ok[i]) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
+      ring[64 * (g0 + i) + lane] = D > 1 ? old[i] : old[i] & 0xffffu;
     }
   }
 }
 
+template <int kDepth>
 __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* data = smem;                                                     // 64 KiB block
   uint32_t* T = reinterpret_cast<uint32_t*>(smem + kBlockSize);             // hash table
-  uint32_t* ring = T + kFTab;                                               // 2 x kRoundPos candidates
+  uint32_t* ring = T + kTabBytes / 4;                             // 2 x kRoundPos candidates
   uint32_t* csize = ring + 2 * kRoundPos;                                   // 2 x 16 chunk infos
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = uniform(tid >> 6);
@@ -210,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   {
     const uint4 z = make_uint4(0, 0, 0, 0);
     uint4* t16 = reinterpret_cast<uint4*>(T);
-    for (uint32_t k = tid; k < kFTab / 4; k += kThreads) t16[k] = z;  // 0 = no position
+    for (uint32_t k = tid; k < kTabBytes / 16; k += kThreads) t16[k] = z;  // 0 = no position
   }
   if (!inserter && kEnd == kChunk && lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
   uint32_t op = 0;
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   const uint32_t rounds = (nchunks + kPW - 1) / kPW;
   // the inserter shares a SIMD with three parse waves and gates every round: issue it first
   if (inserter && SM_FAST_PRIO) __builtin_amdgcn_s_setprio(SM_FAST_PRIO);
-  if (inserter) insert_round(data, T, ring, 0, n, lane);
+  if (inserter) insert_round<kDepth>(data, T, ring, 0, n, lane);
   __syncthreads();
 
   uint64_t w[kP];  // the 8 bytes at each position
@@ -250,7 +252,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     for (int j = 0; j < kP; ++j) ts[j] = wn[j] = 0;
 
     if (inserter) {
-      insert_round(data, T, ring + ((r + 1) & 1) * kRoundPos, (r + 1) * kRoundPos, n, lane);
+      insert_round<kDepth>(data, T, ring + ((r + 1) & 1) * kRoundPos, (r + 1) * kRoundPos, n, lane);
       STAMP(8)
       STAMP_COUNT(10, 1)
     } else if (active) {
@@ -522,19 +524,25 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 }
 #endif
 
-constexpr size_t kFastLds = kBlockSize + 4 * (kFTab + 2 * kRoundPos + 2 * kWavesPerBlock) + kPW * kLevels * kRow;
+constexpr size_t kFastLds = kBlockSize + kTabBytes + 4 * (2 * kRoundPos + 2 * kWavesPerBlock) + kPW * kLevels * kRow;
 static_assert(kFastLds <= 160 * 1024, "fast compressor LDS exceeds a CU");
 
-hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s) {
+template <int D>
+static hipError_t launch_depth(const CompressArgs& a, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_compress_fast, hipFuncAttributeMaxDynamicSharedMemorySize,
+    hipError_t e = hipFuncSetAttribute((const void*)k_compress_fast<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                        (int)kFastLds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_compress_fast, dim3(a.nblk), dim3(kThreads), kFastLds, s, a);
+  hipLaunchKernelGGL(k_compress_fast<D>, dim3(a.nblk), dim3(kThreads), kFastLds, s, a);
   return hipGetLastError();
+}
+
+// mode 1 (SM_MODE_FAST): one chain candidate per position; mode 2 (SM_MODE_FAST_DENSE): two
+hipError_t launch_compress_fast(const CompressArgs& a, int mode, hipStream_t s) {
+  return mode == 2 ? launch_depth<2>(a, s) : launch_depth<1>(a, s);
 }
 
 }  // namespace sm

@@ -32,9 +32,9 @@ struct DecompressArgs {
   uint32_t nblk;
 };
 
-// mode 0 = reference (byte-identical to Snappy.jl), 1 = fast (wave-parallel parse)
+// mode 0 = reference (byte-identical to Snappy.jl), 1 = fast (wave-parallel parse), 2 = fast, denser
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s);
-hipError_t launch_compress_fast(const CompressArgs& a, hipStream_t s);
+hipError_t launch_compress_fast(const CompressArgs& a, int mode, hipStream_t s);
 hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 
 // One large stream decoded in parallel (sm_uncompress): an index pass over 4 KiB chunks of the

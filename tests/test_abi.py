@@ -99,3 +99,13 @@ def test_find_match_length_kat_abi(sm, a, b, limit, expected):
             sm.find_match_length(c, 0, len(a), len(a) + limit - 1)
     else:
         assert sm.find_match_length(c, 0, len(a), len(a) + limit - 1) == expected
+
+
+def test_mode_names_match_header(sm):
+    """The Python mode names map to the header's SM_MODE_* values."""
+    src = open(os.path.join(ROOT, "include", "snappy_mi355x.h")).read()
+    enum = dict((k, int(v)) for k, v in re.findall(r"\b(SM_MODE_[A-Z_]+)\s*=\s*(\d+)", src))
+    assert sm.MODES == {"reference": enum["SM_MODE_REFERENCE"], "fast": enum["SM_MODE_FAST"],
+                        "dense": enum["SM_MODE_FAST_DENSE"]}
+    with pytest.raises(ValueError):
+        sm._mode("turbo")

@@ -111,16 +111,30 @@ def test_reference_mode_fragments_device(sm, oracle, gpu_available):
 
 # ---- fast mode --------------------------------------------------------------------------
 
+FAST_MODES = ["fast", "dense"]
+
+
+@pytest.mark.parametrize("mode", FAST_MODES)
 @pytest.mark.parametrize("fname", ROUNDTRIP_FILES)
-def test_fast_mode_roundtrip_whole_file(sm, oracle, libsnappy, gpu_available, fname):
+def test_fast_mode_roundtrip_whole_file(sm, oracle, libsnappy, gpu_available, fname, mode):
     raw = read_testfile(fname)
-    out = sm.compress(raw, mode="fast")
+    out = sm.compress(raw, mode=mode)
     assert oracle.uncompress(out) == raw
     assert libsnappy.uncompress(out) == raw
     assert sm.uncompress(out) == raw
 
 
-def test_fast_mode_batched_roundtrip(sm, oracle, libsnappy, gpu_available, corpus):
+@pytest.mark.parametrize("mode", FAST_MODES)
+def test_fast_mode_deterministic(sm, gpu_available, corpus, mode):
+    """The parse has no order-dependent state: repeated launches give identical bytes."""
+    blocks = []
+    for raw in corpus.values():
+        blocks.extend(blocks_of(raw))
+    assert sm.compress_batch(blocks, mode=mode) == sm.compress_batch(blocks, mode=mode)
+
+
+@pytest.mark.parametrize("mode", FAST_MODES)
+def test_fast_mode_batched_roundtrip(sm, oracle, libsnappy, gpu_available, corpus, mode):
     rng = np.random.default_rng(5)
     blocks = []
     for raw in corpus.values():
@@ -129,7 +143,7 @@ def test_fast_mode_batched_roundtrip(sm, oracle, libsnappy, gpu_available, corpu
         blocks.append(rng.integers(0, 3, n, dtype=np.uint8).tobytes())
     blocks.append(b"\x00" * 65536)
     blocks.append(rng.integers(0, 256, 65536, dtype=np.uint8).tobytes())
-    outs = sm.compress_batch(blocks, mode="fast")
+    outs = sm.compress_batch(blocks, mode=mode)
     for blk, out in zip(blocks, outs):
         assert oracle.uncompress(out) == blk
         assert libsnappy.uncompress(out) == blk

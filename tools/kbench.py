@@ -30,6 +30,7 @@ def main():
     torch.cuda.synchronize()
     ops = {
         "compress_fast": lambda: b.compress(sm, "fast"),
+        "compress_dense": lambda: b.compress(sm, "dense"),
         "compress_ref": lambda: b.compress(sm, "reference"),
         "uncompress": lambda: b.uncompress(sm),
     }
