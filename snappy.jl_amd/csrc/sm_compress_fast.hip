@@ -22,9 +22,14 @@
 //    chunks -- literal runs that cross chunk boundaries are merged -- and the emission: token
 //    lanes write tag bytes, position lanes scatter literal bytes.
 // One barrier per round (chunk infos are double-buffered).  Output is deterministic.
+#include <type_traits>
+
 #include "sm_device.h"
 #include "sm_internal.h"
 
+#ifndef SM_FAST_SHFL
+#define SM_FAST_SHFL 0
+#endif
 #ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches, 4 inserter only
 #define SM_ABLATE 0
 #endif
@@ -53,7 +58,6 @@ constexpr uint32_t kTabBytes = 4u << kTabBits;
 constexpr uint32_t kWavesPerBlock = 16;
 constexpr uint32_t kPW = kWavesPerBlock - 1;  // parse waves; wave kPW is the inserter
 constexpr uint32_t kThreads = 64 * kWavesPerBlock;
-constexpr uint32_t kRoundPos = kPW * kChunk;  // positions per round
 // J0..J_{kLevels-1}: a chunk holds <= kChunk/4 copies, so its walk takes < kChunk/4 steps
 constexpr uint32_t kLevels = kChunk == 256 ? 6 : 5;
 // the chain's end marker: the chunk end (128 fits a byte); for 256-byte chunks position 255,
@@ -128,21 +132,38 @@ __device__ inline uint32_t fast_hash(uint32_t w) {
   return (p >> 10) & ((1u << kBits) - 1);
 }
 
+// Round geometry per mode.  SM_MODE_FAST (depth 1) keeps u16 candidates and gives each parse
+// wave two chunks per round (30 chunks, 7680 positions: half the rounds, so half the barrier
+// tails and round layouts per byte); SM_MODE_FAST_DENSE (depth 2) keeps u32 candidate pairs,
+// which leave LDS for one chunk per wave (15 chunks, 3840 positions).  Both rings are 30 KiB.
+template <int D>
+struct Cfg {
+#ifndef SM_FAST_CPW
+#define SM_FAST_CPW 2
+#endif
+  static constexpr int kCPW = D == 1 ? SM_FAST_CPW : 1;  // chunks per parse wave per round
+  static constexpr uint32_t kSlots = kPW * kCPW;         // chunks per round
+  static constexpr uint32_t kRoundPos = kSlots * kChunk; // positions per round
+  typedef typename std::conditional<D == 1, uint16_t, uint32_t>::type Cand;
+  static constexpr uint32_t kRingBytes = 2 * kRoundPos * sizeof(Cand);
+};
+
 // Inserter: positions [r0, r0 + kRoundPos) in order; ring[i] receives the candidates of
 // position r0 + i (the old table entry).  kG groups of 64 positions per step so the LDS round
 // trips overlap.  r0 is a multiple of 64: the words come from aligned dwords (immediate
 // offsets), and reads past n stay inside the LDS allocation (the table follows the block).
 template <int D>
-__device__ inline void insert_round(const uint8_t* data, uint32_t* T, uint32_t* ring, uint32_t r0, uint32_t n,
-                                    uint32_t lane) {
+__device__ inline void insert_round(const uint8_t* data, uint32_t* T, typename Cfg<D>::Cand* ring, uint32_t r0,
+                                    uint32_t n, uint32_t lane) {
 #ifndef SM_FAST_KG
 #define SM_FAST_KG 6
 #endif
   constexpr int kG = SM_FAST_KG;
-  static_assert((kRoundPos / 64) % kG == 0, "insert step");
+  constexpr uint32_t kRP = Cfg<D>::kRoundPos;
+  static_assert((kRP / 64) % kG == 0, "insert step");
   if (r0 >= n) return;
-  const uint32_t ngroups = min((n - r0 + 63) >> 6, kRoundPos / 64);
-  const bool full = r0 + kRoundPos + 3 <= n;  // every position of the round has its 4 bytes
+  const uint32_t ngroups = min((n - r0 + 63) >> 6, kRP / 64);
+  const bool full = r0 + kRP + 3 <= n;  // every position of the round has its 4 bytes
   const uint32_t sh = lane & 3u;
   for (uint32_t g0 = 0; g0 < ngroups; g0 += kG) {
     const uint32_t base = r0 + 64 * g0;
@@ -163,23 +184,229 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, uint32_t* 
     for (int i = 0; i < kG; ++i) {
       // the old latest becomes the second-latest (the new entry's high half)
       if (D > 1 && ok[i]) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
-      ring[64 * (g0 + i) + lane] = D > 1 ? old[i] : old[i] & 0xffffu;
+      ring[64 * (g0 + i) + lane] = (typename Cfg<D>::Cand)old[i];
     }
+  }
+}
+
+// A parsed chunk, held in registers from its parse to its emission after the round barrier.
+struct ChunkTok {
+  uint32_t c0, ce;           // the chunk's positions [c0, ce); ce == c0: no chunk
+  uint32_t ta, tb;           // token in lane t: copy position | length << 16; offset
+  uint32_t ntok, incl, sz;   // tokens; inclusive scan of token sizes; this lane's token size
+  uint32_t litlen, littag, ls;  // the token's literal run: length, tag bytes, start
+  uint64_t ts[kP];           // copy-start bitmask of the chunk's positions
+};
+
+// Parse of chunk [c0, ce) (ce > c0) from its ring candidates cr; returns the chunk info word
+// for the round layout: unmerged size | leading literal piece << 11 | trailing literal piece
+// << 20 | no copies at all << 29.
+template <int kDepth>
+__device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<kDepth>::Cand* cr, uint8_t* jt, uint64_t* tsw,
+                                       uint32_t c0, uint32_t ce, uint32_t n, uint32_t lane, ChunkTok& t) {
+  t.c0 = c0;
+  t.ce = ce;
+  t.ta = t.tb = t.ntok = t.incl = t.sz = t.litlen = t.littag = t.ls = 0;
+#pragma unroll
+  for (int j = 0; j < kP; ++j) t.ts[j] = 0;
+  // (a) candidates: the latest (and second-latest) earlier position with the same hash,
+  // verified and extended 8 bytes at a time; the longest wins (ties: the latest).
+  uint32_t Ls[kP], offs[kP];
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const uint32_t q = c0 + 64 * j + lane;
+    const uint64_t wq = lds_ld64(data, q < n ? q : 0);  // the 8 bytes at q
+    const bool can = q + 4 <= ce;
+    const uint32_t cv = cr[64 * j + lane];
+    uint32_t L = 0, c = q;
+#pragma unroll
+    for (int i = 0; i < kDepth; ++i) {
+      const uint32_t p = (cv >> (16 * i)) & 0xffffu;  // position + 1, 0 = none
+      if (can && p != 0 && p - 1 < q) {
+        const uint64_t x = lds_ld64(data, p - 1) ^ wq;
+        const uint32_t l = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
+        if (l >= 4 && l > L) {
+          L = l;
+          c = p - 1;
+        }
+      }
+    }
+    Ls[j] = min(L, ce - q);
+    offs[j] = q - c;
+  }
+  // finish matches that filled the 8-byte window: 8 bytes per lane per step
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const uint32_t q = c0 + 64 * j + lane;
+    uint32_t L = Ls[j];
+    bool more = L >= 8 && q + L < ce;
+    while (ballot(more)) {
+      if (more) {
+        const uint32_t avail = ce - q - L;
+        const uint64_t x = lds_ld64(data, q - offs[j] + L) ^ lds_ld64(data, q + L);
+        const uint32_t fb = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
+        L += min(fb, avail);
+        more = fb == 8 && avail > 8;
+      }
+    }
+    Ls[j] = (SM_ABLATE & 2) ? 0u : L;
+  }
+  // Greedy parse by pointer doubling (no serial loop) over the chunk's positions.  J0 skips
+  // literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a non-match), else
+  // kEnd, so the greedy walk from 0 steps only between copies; J_k = J_{k-1} o J_{k-1}.  Chain
+  // element t of the chunk is then computed directly in lane t from the jump tables.  No
+  // copies at all (incompressible): no parse.
+  uint64_t M[kP];
+  uint64_t any = 0;
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    M[j] = ballot(Ls[j] != 0);
+    any |= M[j];
+  }
+  uint32_t nmatch = 0, last_end = 0;
+  if (any) {
+    // F[i]: the first match position in words > i (kEnd: none)
+    uint32_t F[kP];
+    F[kP - 1] = kEnd;
+#pragma unroll
+    for (int i = kP - 2; i >= 0; --i) F[i] = M[i + 1] ? 64u * (i + 1) + ctz64(M[i + 1]) : F[i + 1];
+    uint32_t jv[kP];
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const uint32_t rr = 64 * j + lane;
+      const uint32_t x = rr + Ls[j];  // <= kChunk: copies end inside the chunk
+      const uint32_t i = x >> 6;
+      uint64_t mw = M[0];
+#pragma unroll
+      for (int u = 1; u < kP; ++u) mw = i == (uint32_t)u ? M[u] : mw;
+      uint32_t f = kEnd;
+#pragma unroll
+      for (int u = 0; u < kP; ++u) f = i == (uint32_t)u ? F[u] : f;
+      const uint64_t m = i < (uint32_t)kP ? mw >> (x & 63u) : 0;
+      jv[j] = m ? x + ctz64(m) : f;
+      jt[rr] = (uint8_t)jv[j];
+    }
+#pragma unroll
+    for (int kk = 1; kk < (int)kLevels; ++kk) {
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+      for (int j = 0; j < kP; ++j) {
+        jv[j] = jt[(kk - 1) * kRow + jv[j]];
+        jt[kk * kRow + 64 * j + lane] = (uint8_t)jv[j];
+      }
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    // chain element t (lane t < kChunk/4) from position 0: J_k for every set bit k of t.
+    // Only element 0 can be a non-match (J0 jumps to match positions), the rest are the
+    // copies; past the last copy the chain sits at kEnd (no match).
+    uint32_t c = 0;
+#pragma unroll
+    for (int kk = 0; kk < (int)kLevels; ++kk) {
+      const uint32_t tt = jt[kk * kRow + c];
+      c = ((lane >> kk) & 1u) ? tt : c;
+    }
+    // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles of
+    // length | offset << 9
+    const uint32_t ci = c & 63u, cj = c >> 6;
+    uint32_t vc = 0;
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const uint32_t v = __shfl(Ls[j] | (offs[j] << 9), ci, 64);
+      vc = cj == (uint32_t)j ? v : vc;
+    }
+    const uint32_t Lc = c < kEnd ? vc & 0x1ffu : 0u;
+    const bool istok = lane < kChunk / 4 && Lc != 0;
+    const uint64_t tm = ballot(istok);
+    nmatch = (uint32_t)__builtin_popcountll(tm);
+    const uint32_t sh = (uint32_t)(tm & 1u) ^ 1u;  // tokens start at lane 1 if 0 is no match
+    // token: position | length << 16; offset
+    const uint32_t tav = __shfl(c | (Lc << 16), lane + sh, 64), tbv = __shfl(vc >> 9, lane + sh, 64);
+    if (nmatch) {
+      t.ta = tav;
+      t.tb = tbv;
+      last_end = readlane(c + Lc, nmatch - 1 + sh);
+    }
+    // copy-start bitmask (position p of the chunk) for the literal scatter
+    if (lane < kP) tsw[lane] = 0;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (istok)
+      __hip_atomic_fetch_or(&tsw[c >> 6], 1ull << (c & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+    for (int j = 0; j < kP; ++j) t.ts[j] = tsw[j];
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the next chunk's jump tables follow these reads
+  }
+  t.ntok = nmatch;
+  if (last_end < ce - c0) {  // trailing literal run: a token without a copy
+    const bool me = lane == t.ntok;
+    t.ta = me ? ce - c0 : t.ta;
+    t.tb = me ? 0u : t.tb;
+    ++t.ntok;
+  }
+  const uint32_t tq = c0 + (t.ta & 0xffff), tL = t.ta >> 16;
+  const uint32_t end = tq + tL;
+  const uint32_t prev_end = __builtin_amdgcn_update_dpp(0u, end, 0x138, 0xf, 0xf, false);  // wave_shr:1
+  t.ls = lane == 0 ? c0 : prev_end;
+  if (lane < t.ntok) {
+    t.litlen = tq - t.ls;
+    t.littag = lit_tag_bytes(t.litlen);
+    t.sz = t.littag + t.litlen + (tL ? copy_bytes_cf(t.tb, tL) : 0);
+  }
+  t.incl = scan_dpp(t.sz);
+  const uint32_t trail = ce - c0 - last_end;
+  return readlane(t.incl, t.ntok - 1) | (readlane(t.litlen, 0) << 11) | (trail << 20) | ((nmatch == 0) << 29);
+}
+
+// Emission of a parsed chunk at output offset o0 (its place in the round): token lanes write
+// tag bytes, position lanes scatter literal bytes.  mycont: the chunk's leading literal
+// continues the previous chunk's run (its tag is dropped); myrun: the chunk's trailing run
+// spans later chunks and its tag encodes that whole length.
+__device__ inline void emit_chunk(uint8_t* dst, const uint8_t* data, const ChunkTok& t, uint32_t o0, uint32_t mycont,
+                                  uint32_t myrun, uint32_t lane) {
+  const uint32_t rm = mycont ? readlane(t.littag, 0) : 0u;  // leading tag removed
+  const uint32_t tq = t.c0 + (t.ta & 0xffff), tL = t.ta >> 16;
+  const uint32_t o = o0 + t.incl - t.sz - (lane > 0 ? rm : 0u);
+  uint32_t mytag = (lane == 0 && mycont) ? 0u : t.littag, tagv = t.litlen;
+  if (myrun && lane == t.ntok - 1) {  // the run's trailing token
+    mytag = lit_tag_bytes(myrun);
+    tagv = myrun;
+  }
+  if (lane < t.ntok) {
+    put_lit_tag(dst, o, mytag, tagv);
+    if (tL) put_copy_cf(dst, o + mytag + t.litlen, t.tb, tL);
+  }
+  const uint32_t delta = o + mytag - t.ls;  // output - input position of the run (mod 2^32)
+  const uint32_t end = tq + tL;
+  uint32_t below = 0;
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const uint32_t x = t.c0 + 64 * j + lane;
+    uint32_t cnt = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(t.ts[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)t.ts[j], 0u));
+    cnt += (uint32_t)(t.ts[j] >> lane) & 1u;  // tokens whose copy starts at or before x
+    const uint32_t pend = __shfl(end, cnt ? cnt - 1 : 0, 64);
+    const uint32_t dl = __shfl(delta, cnt, 64);
+    if (x < t.ce && (cnt == 0 || x >= pend)) dst[x + dl] = data[x];  // 32-bit offset: saddr store
+    below += __builtin_popcountll(t.ts[j]);
   }
 }
 
 template <int kDepth>
 __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
+  typedef Cfg<kDepth> C;
+  typedef typename C::Cand Cand;
+  constexpr uint32_t kSlots = C::kSlots, kRP = C::kRoundPos;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* data = smem;                                                     // 64 KiB block
   uint32_t* T = reinterpret_cast<uint32_t*>(smem + kBlockSize);             // hash table
-  uint32_t* ring = T + kTabBytes / 4;                             // 2 x kRoundPos candidates
-  uint32_t* csize = ring + 2 * kRoundPos;                                   // 2 x 16 chunk infos
+  Cand* ring = reinterpret_cast<Cand*>(T + kTabBytes / 4);                  // 2 x kRoundPos candidates
+  uint32_t* csize = reinterpret_cast<uint32_t*>(ring + 2 * kRP);            // 2 x 32 chunk infos
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = uniform(tid >> 6);
   const uint32_t lane = tid & 63;
   const bool inserter = wave == kPW;
-  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + 2 * kWavesPerBlock) + (inserter ? 0 : wave) * kLevels * kRow;
+  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + 64) + (inserter ? 0 : wave) * kLevels * kRow;
+  uint64_t* tsw = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(csize + 64) + kPW * kLevels * kRow) +
+                  (inserter ? 0 : wave) * kP;  // per-wave copy-start bitmask
 
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.in_len[b];
@@ -224,201 +451,41 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   __syncthreads();
 
   const uint32_t nchunks = (n + kChunk - 1) / kChunk;
-  const uint32_t rounds = (nchunks + kPW - 1) / kPW;
+  const uint32_t rounds = (nchunks + kSlots - 1) / kSlots;
   // the inserter shares a SIMD with three parse waves and gates every round: issue it first
   if (inserter && SM_FAST_PRIO) __builtin_amdgcn_s_setprio(SM_FAST_PRIO);
   if (inserter) insert_round<kDepth>(data, T, ring, 0, n, lane);
   __syncthreads();
 
-  uint64_t w[kP];  // the 8 bytes at each position
-  if (!inserter) {
-#pragma unroll
-    for (int j = 0; j < kP; ++j) {
-      uint32_t q = wave * kChunk + 64 * j + lane;
-      w[j] = lds_ld64(data, q < n ? q : 0);
-    }
-  }
-
   STAMP_DECL
   for (uint32_t r = 0; r < rounds; ++r) {
-    const uint32_t k = r * kPW + wave;
-    const bool active = !inserter && k < nchunks && !(SM_ABLATE & 4);
-    const uint32_t c0 = k * kChunk;
-    const uint32_t ce = active ? min(c0 + kChunk, n) : c0;
-    uint32_t* cinfo = csize + (r & 1) * kWavesPerBlock;
-    uint32_t ta = 0, tb = 0, ntok = 0, incl = 0, sz = 0, litlen = 0, littag = 0, ls = 0;
-    uint64_t ts[kP], wn[kP];
-#pragma unroll
-    for (int j = 0; j < kP; ++j) ts[j] = wn[j] = 0;
-
+#if SM_FAST_XBAR
+    __syncthreads();
+#endif
+    uint32_t* cinfo = csize + (r & 1) * 32;
+    ChunkTok tk[C::kCPW];
     if (inserter) {
-      insert_round<kDepth>(data, T, ring + ((r + 1) & 1) * kRoundPos, (r + 1) * kRoundPos, n, lane);
+      insert_round<kDepth>(data, T, ring + ((r + 1) & 1) * kRP, (r + 1) * kRP, n, lane);
       STAMP(8)
       STAMP_COUNT(10, 1)
-    } else if (active) {
-      STAMP_COUNT(11, 1)
-      // (a) candidates: the latest (and second-latest) earlier position with the same hash,
-      // verified and extended 8 bytes at a time; the longest wins (ties: the latest).
-      const uint32_t* cr = ring + (r & 1) * kRoundPos + wave * kChunk;
-      uint32_t Ls[kP], offs[kP];
+    } else {
+      // parse wave w owns the round's chunk slots w, w + 15, ...
 #pragma unroll
-      for (int j = 0; j < kP; ++j) {
-        const uint32_t q = c0 + 64 * j + lane;
-        const bool can = q + 4 <= ce;
-        const uint32_t cv = cr[64 * j + lane];
-        uint32_t L = 0, c = q;
-#pragma unroll
-        for (int i = 0; i < kDepth; ++i) {
-          const uint32_t p = (cv >> (16 * i)) & 0xffffu;  // position + 1, 0 = none
-          if (can && p != 0 && p - 1 < q) {
-            const uint64_t x = lds_ld64(data, p - 1) ^ w[j];
-            const uint32_t l = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
-            if (l >= 4 && l > L) {
-              L = l;
-              c = p - 1;
-            }
-          }
+      for (int u = 0; u < C::kCPW; ++u) {
+        const uint32_t slot = wave + kPW * u;
+        const uint32_t k = r * kSlots + slot;
+        const uint32_t c0 = k * kChunk;
+        if (k < nchunks && !(SM_ABLATE & 4)) {
+          STAMP_COUNT(11, 1)
+          const uint32_t info = parse_chunk<kDepth>(data, ring + (r & 1) * kRP + slot * kChunk, jt, tsw, c0,
+                                                    min(c0 + kChunk, n), n, lane, tk[u]);
+          if (lane == 0) cinfo[slot] = info;
+        } else {
+          tk[u].c0 = tk[u].ce = c0;
+          if (lane == 0) cinfo[slot] = 0;
         }
-        Ls[j] = min(L, ce - q);
-        offs[j] = q - c;
-      }
-      STAMP(0)
-      // finish matches that filled the 8-byte window: 8 bytes per lane per step
-#pragma unroll
-      for (int j = 0; j < kP; ++j) {
-        const uint32_t q = c0 + 64 * j + lane;
-        uint32_t L = Ls[j];
-        bool more = L >= 8 && q + L < ce;
-        while (ballot(more)) {
-          if (more) {
-            const uint32_t avail = ce - q - L;
-            const uint64_t x = lds_ld64(data, q - offs[j] + L) ^ lds_ld64(data, q + L);
-            const uint32_t fb = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
-            L += min(fb, avail);
-            more = fb == 8 && avail > 8;
-          }
-        }
-        Ls[j] = (SM_ABLATE & 2) ? 0u : L;
-      }
-      STAMP(1)
-      // Greedy parse by pointer doubling (no serial loop) over the chunk's positions.  J0
-      // skips literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a
-      // non-match), else kEnd, so the greedy walk from 0 steps only between copies;
-      // J_k = J_{k-1} o J_{k-1}.  Chain element t of the chunk is then computed directly in
-      // lane t from the jump tables.  No copies at all (incompressible): no parse.
-      uint64_t M[kP];
-      uint64_t any = 0;
-#pragma unroll
-      for (int j = 0; j < kP; ++j) {
-        M[j] = ballot(Ls[j] != 0);
-        any |= M[j];
-      }
-      uint32_t nmatch = 0, last_end = 0;
-      if (any) {
-        // F[i]: the first match position in words > i (kEnd: none)
-        uint32_t F[kP];
-        F[kP - 1] = kEnd;
-#pragma unroll
-        for (int i = kP - 2; i >= 0; --i) F[i] = M[i + 1] ? 64u * (i + 1) + ctz64(M[i + 1]) : F[i + 1];
-        uint32_t jv[kP];
-#pragma unroll
-        for (int j = 0; j < kP; ++j) {
-          const uint32_t rr = 64 * j + lane;
-          const uint32_t x = rr + Ls[j];  // <= kChunk: copies end inside the chunk
-          const uint32_t i = x >> 6;
-          uint64_t mw = M[0];
-#pragma unroll
-          for (int t = 1; t < kP; ++t) mw = i == (uint32_t)t ? M[t] : mw;
-          uint32_t f = kEnd;
-#pragma unroll
-          for (int t = 0; t < kP; ++t) f = i == (uint32_t)t ? F[t] : f;
-          const uint64_t m = i < (uint32_t)kP ? mw >> (x & 63u) : 0;
-          jv[j] = m ? x + ctz64(m) : f;
-          jt[rr] = (uint8_t)jv[j];
-        }
-#pragma unroll
-        for (int kk = 1; kk < (int)kLevels; ++kk) {
-          __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#pragma unroll
-          for (int j = 0; j < kP; ++j) {
-            jv[j] = jt[(kk - 1) * kRow + jv[j]];
-            jt[kk * kRow + 64 * j + lane] = (uint8_t)jv[j];
-          }
-        }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        // chain element t (lane t < kChunk/4) from position 0: J_k for every set bit k of t.
-        // Only element 0 can be a non-match (J0 jumps to match positions), the rest are the
-        // copies; past the last copy the chain sits at kEnd (no match).
-        uint32_t c = 0;
-#pragma unroll
-        for (int kk = 0; kk < (int)kLevels; ++kk) {
-          const uint32_t t = jt[kk * kRow + c];
-          c = ((lane >> kk) & 1u) ? t : c;
-        }
-        // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles of
-        // length | offset << 9
-        const uint32_t ci = c & 63u, cj = c >> 6;
-        uint32_t vc = 0;
-#pragma unroll
-        for (int j = 0; j < kP; ++j) {
-          const uint32_t v = __shfl(Ls[j] | (offs[j] << 9), ci, 64);
-          vc = cj == (uint32_t)j ? v : vc;
-        }
-        const uint32_t Lc = c < kEnd ? vc & 0x1ffu : 0u;
-        const bool istok = lane < kChunk / 4 && Lc != 0;
-        const uint64_t tm = ballot(istok);
-        nmatch = (uint32_t)__builtin_popcountll(tm);
-        const uint32_t sh = (uint32_t)(tm & 1u) ^ 1u;  // tokens start at lane 1 if 0 is no match
-        // token: position | length << 16; offset
-        const uint32_t tav = __shfl(c | (Lc << 16), lane + sh, 64), tbv = __shfl(vc >> 9, lane + sh, 64);
-        if (nmatch) {
-          ta = tav;
-          tb = tbv;
-          last_end = readlane(c + Lc, nmatch - 1 + sh);
-        }
-        // copy-start bitmask (position p of the chunk) for the literal scatter
-        uint64_t* tsw = reinterpret_cast<uint64_t*>(jt);
-        if (lane < kP) tsw[lane] = 0;
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (istok)
-          __hip_atomic_fetch_or(&tsw[c >> 6], 1ull << (c & 63u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#pragma unroll
-        for (int j = 0; j < kP; ++j) ts[j] = tsw[j];
-      }
-      STAMP(2)
-      ntok = nmatch;
-      if (last_end < ce - c0) {  // trailing literal run: a token without a copy
-        const bool me = lane == ntok;
-        ta = me ? ce - c0 : ta;
-        tb = me ? 0u : tb;
-        ++ntok;
-      }
-      const uint32_t tq = c0 + (ta & 0xffff), tL = ta >> 16;
-      const uint32_t end = tq + tL;
-      const uint32_t prev_end = __builtin_amdgcn_update_dpp(0u, end, 0x138, 0xf, 0xf, false);  // wave_shr:1
-      ls = lane == 0 ? c0 : prev_end;
-      if (lane < ntok) {
-        litlen = tq - ls;
-        littag = lit_tag_bytes(litlen);
-        sz = littag + litlen + (tL ? copy_bytes_cf(tb, tL) : 0);
-      }
-      incl = scan_dpp(sz);
-      // chunk info for the round layout: unmerged size | leading literal piece << 11 |
-      // trailing literal piece << 20 | no copies at all << 29
-      const uint32_t trail = ce - c0 - last_end;
-      if (lane == 0)
-        cinfo[wave] = readlane(incl, ntok - 1) | (readlane(litlen, 0) << 11) | (trail << 20) | ((nmatch == 0) << 29);
-      // next round's words
-      const uint32_t c2 = (k + kPW) * kChunk;
-#pragma unroll
-      for (int j = 0; j < kP; ++j) {
-        const uint32_t q = c2 + 64 * j + lane;
-        wn[j] = lds_ld64(data, q < n ? q : 0);
       }
       STAMP(3)
-    } else {
-      if (lane == 0) cinfo[wave] = 0;
     }
     __syncthreads();  // the round's chunk infos; the next round's candidates
     if (inserter) {
@@ -427,81 +494,75 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     }
     STAMP(4)
 
-    // (c) round layout, lane-parallel over the round's chunks (lane u = chunk u): a literal
-    // run that crosses chunk boundaries inside the round is emitted once, with one tag for
-    // its total length in the chunk where it starts (runs restart at round boundaries).
+    // (c) round layout, lane-parallel over the round's chunks (lane u = chunk slot u): a
+    // literal run that crosses chunk boundaries inside the round is emitted once, with one
+    // tag for its total length in the chunk where it starts (runs restart at round boundaries).
     //   cont_in[u]: chunk u's leading literal piece continues chunk u-1's trailing piece (no tag)
     //   mid[u]:     chunk u is all literal and continues a run (no tag of its own)
     //   start[u]:   chunk u's trailing piece starts a run; if cont_in[u+1] the run spans chunks
     //               and its tag encodes the run length up to the end of the last piece.
-    uint32_t myb, mycont, myrun, total;
+    uint32_t inclm, Smv, contv, runv, total;
     {
-      static_assert(kPW < 16, "the round layout runs in DPP row 0");
-      const uint32_t info = lane < kPW ? cinfo[lane] : 0u;
+      const uint32_t info = lane < kSlots ? cinfo[lane] : 0u;
       const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0x1ffu, trl = (info >> 20) & 0x1ffu;
       const bool nocp = (info >> 29) & 1u;
-      const uint32_t trl_prev = __builtin_amdgcn_update_dpp(0u, trl, 0x111, 0xf, 0xf, true);  // row_shr:1
-      const bool cont_in = lane > 0 && lane < kPW && trl_prev > 0 && lead > 0;
+#if SM_FAST_SHFL
+      const uint32_t trl_prev = lane ? __shfl_up(trl, 1, 64) : 0u;
+#else
+      const uint32_t trl_prev = __builtin_amdgcn_update_dpp(0u, trl, 0x138, 0xf, 0xf, false);  // wave_shr:1
+#endif
+      const bool cont_in = lane > 0 && lane < kSlots && trl_prev > 0 && lead > 0;
       const bool mid = nocp && cont_in;
       const bool start = trl > 0 && !mid;
-      const bool cont_next = __builtin_amdgcn_update_dpp(0u, (uint32_t)cont_in, 0x101, 0xf, 0xf, true) != 0;  // row_shl:1
-      const uint32_t cu = (r * kPW + lane) * kChunk;                         // chunk start
+#if SM_FAST_SHFL
+      const bool cont_next = __shfl_down((uint32_t)cont_in, 1, 64) != 0 && lane < 63;
+#else
+      const bool cont_next = __builtin_amdgcn_update_dpp(0u, (uint32_t)cont_in, 0x130, 0xf, 0xf, false) != 0;  // wave_shl:1
+#endif
+      const uint32_t cu = (r * kSlots + lane) * kChunk;                      // chunk start
       const uint32_t ceu = min(cu + kChunk, n);
       // the run ending in chunk u ends at cu + lead; a run starting in chunk v ends in the
       // first later chunk whose piece ends it (suffix min over lanes)
       const bool ends = cont_in && !(mid && cont_next);
       uint32_t nxt = ends ? lane : 0xffu;
-      nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x101, 0xf, 0xf, false));  // row_shl:1
-      nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x102, 0xf, 0xf, false));  // row_shl:2
-      nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x104, 0xf, 0xf, false));  // row_shl:4
-      nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x108, 0xf, 0xf, false));  // row_shl:8
-      nxt = __builtin_amdgcn_update_dpp(0xffu, nxt, 0x101, 0xf, 0xf, false);                       // first end after u
+      if (kSlots < 16) {  // one DPP row
+        nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x101, 0xf, 0xf, false));  // row_shl:1
+        nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x102, 0xf, 0xf, false));  // row_shl:2
+        nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x104, 0xf, 0xf, false));  // row_shl:4
+        nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x108, 0xf, 0xf, false));  // row_shl:8
+      } else {
+#pragma unroll
+        for (uint32_t d = 1; d < kSlots; d <<= 1) {
+          const uint32_t o2 = __shfl_down(nxt, d, 64);
+          nxt = (lane + d < kSlots && o2 < nxt) ? o2 : nxt;
+        }
+      }
+#if SM_FAST_SHFL
+      nxt = lane < 63 ? __shfl_down(nxt, 1, 64) : 0xffu;
+#else
+      nxt = __builtin_amdgcn_update_dpp(0xffu, nxt, 0x130, 0xf, 0xf, false);                       // first end after u
+#endif
       const uint32_t endpos = __shfl(cu + lead, nxt & 63u, 64);
       const uint32_t runlen = (start && cont_next) ? endpos - (ceu - trl) : 0u;
       const uint32_t Sm = S - (cont_in ? lit_tag_bytes(lead) : 0u) +
                           (runlen ? lit_tag_bytes(runlen) - lit_tag_bytes(trl) : 0u);
-      uint32_t inclm = lane < kPW ? Sm : 0u;
-      inclm += __builtin_amdgcn_update_dpp(0u, inclm, 0x111, 0xf, 0xf, true);  // row_shr:1
-      inclm += __builtin_amdgcn_update_dpp(0u, inclm, 0x112, 0xf, 0xf, true);  // row_shr:2
-      inclm += __builtin_amdgcn_update_dpp(0u, inclm, 0x114, 0xf, 0xf, true);  // row_shr:4
-      inclm += __builtin_amdgcn_update_dpp(0u, inclm, 0x118, 0xf, 0xf, true);  // row_shr:8
-      total = readlane(inclm, kPW - 1);
-      myb = readlane(inclm - Sm, wave);
-      mycont = readlane((uint32_t)cont_in, wave);
-      myrun = readlane(runlen, wave);
+      inclm = scan_dpp(lane < kSlots ? Sm : 0u);
+      total = readlane(inclm, kSlots - 1);
+      Smv = Sm;
+      contv = cont_in;
+      runv = runlen;
     }
     STAMP(5)
-    if (active && !(SM_ABLATE & 1)) {
-      const uint32_t rm = mycont ? readlane(littag, 0) : 0u;                 // leading tag removed
-      const uint32_t tq = c0 + (ta & 0xffff), tL = ta >> 16;
-      const uint32_t o = op + myb + incl - sz - (lane > 0 ? rm : 0u);
-      uint32_t mytag = (lane == 0 && mycont) ? 0u : littag, tagv = litlen;
-      if (myrun && lane == ntok - 1) {                                       // the run's trailing token
-        mytag = lit_tag_bytes(myrun);
-        tagv = myrun;
-      }
-      if (lane < ntok) {
-        put_lit_tag(dst, o, mytag, tagv);
-        if (tL) put_copy_cf(dst, o + mytag + litlen, tb, tL);
-      }
-      const int32_t delta = (int32_t)(o + mytag) - (int32_t)ls;
-      const uint32_t end = tq + tL;
-      uint32_t below = 0;
+    if (!(SM_ABLATE & 1)) {
 #pragma unroll
-      for (int j = 0; j < kP; ++j) {
-        const uint32_t x = c0 + 64 * j + lane;
-        uint32_t cnt = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(ts[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)ts[j], 0u));
-        cnt += (uint32_t)(ts[j] >> lane) & 1u;  // tokens whose copy starts at or before x
-        const uint32_t pend = __shfl(end, cnt ? cnt - 1 : 0, 64);
-        const int32_t dl = __shfl(delta, cnt, 64);
-        if (x < ce && (cnt == 0 || x >= pend)) dst[(int32_t)x + dl] = (uint8_t)w[j];
-        below += __builtin_popcountll(ts[j]);
+      for (int u = 0; u < C::kCPW; ++u) {
+        const uint32_t slot = wave + kPW * u;
+        if (tk[u].ce > tk[u].c0)
+          emit_chunk(dst, data, tk[u], op + readlane(inclm - Smv, slot), readlane(contv, slot), readlane(runv, slot), lane);
       }
     }
     STAMP(6)
     op += total;
-#pragma unroll
-    for (int j = 0; j < kP; ++j) w[j] = wn[j];
   }
   STAMP(7)
   STAMP_FLUSH(g_stamp_c)
@@ -524,19 +585,22 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 }
 #endif
 
-constexpr size_t kFastLds = kBlockSize + kTabBytes + 4 * (2 * kRoundPos + 2 * kWavesPerBlock) + kPW * kLevels * kRow;
-static_assert(kFastLds <= 160 * 1024, "fast compressor LDS exceeds a CU");
+template <int D>
+constexpr size_t fast_lds() {
+  return kBlockSize + kTabBytes + Cfg<D>::kRingBytes + 4 * 64 + kPW * kLevels * kRow + kPW * 8 * kP;
+}
+static_assert(fast_lds<1>() <= 160 * 1024 && fast_lds<2>() <= 160 * 1024, "fast compressor LDS exceeds a CU");
 
 template <int D>
 static hipError_t launch_depth(const CompressArgs& a, hipStream_t s) {
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)k_compress_fast<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)kFastLds);
+                                       (int)fast_lds<D>());
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(k_compress_fast<D>, dim3(a.nblk), dim3(kThreads), kFastLds, s, a);
+  hipLaunchKernelGGL(k_compress_fast<D>, dim3(a.nblk), dim3(kThreads), fast_lds<D>(), s, a);
   return hipGetLastError();
 }
 

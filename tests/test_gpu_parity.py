@@ -139,8 +139,12 @@ def test_fast_mode_batched_roundtrip(sm, oracle, libsnappy, gpu_available, corpu
     blocks = []
     for raw in corpus.values():
         blocks.extend(blocks_of(raw))
-    for n in list(range(0, 70)) + [65535, 65536]:
+    # sizes at the parse's chunk (256 B) and round (15 x 256 B) boundaries
+    edges = [k * m + d for m in (256, 3840) for k in (1, 2, 17) for d in (-1, 0, 1) if 0 < k * m + d <= 65536]
+    for n in list(range(0, 70)) + edges + [65535, 65536]:
         blocks.append(rng.integers(0, 3, n, dtype=np.uint8).tobytes())
+    for n in edges[:6]:
+        blocks.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
     blocks.append(b"\x00" * 65536)
     blocks.append(rng.integers(0, 256, 65536, dtype=np.uint8).tobytes())
     outs = sm.compress_batch(blocks, mode=mode)

@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 NAMES = ["ring+flush", "walk", "decode", "longlit", "in-order tail", "big literals", "", "", "round"]
-CNAMES = ["candidates", "long matches", "parse", "tokens+sizes", "barrier wait", "layout", "emission", "tail"]
+CNAMES = ["", "", "", "parse (all chunks)", "barrier wait", "layout", "emission", "tail"]
 INAMES = ["inserter: inserts", "inserter: barrier wait"]
 
 
@@ -84,10 +84,11 @@ def compress_stamps(args):
     v = list(buf)
     rounds, irounds = v[11], v[10]
     tot = sum(v[:8])
-    print("compress_fast %s: %d parse wave-rounds, %d inserter rounds" % (args.data, rounds, irounds))
+    print("compress_fast %s: %d parsed chunks, %d inserter rounds" % (args.data, rounds, irounds))
     for i, nme in enumerate(CNAMES):
-        print("  %-24s %5.1f%%  %7.0f cycles/wave-round" % (nme, 100.0 * v[i] / tot, v[i] / max(rounds, 1)))
-    print("  total (parse waves)      %7.0f cycles/wave-round" % (tot / max(rounds, 1)))
+        if nme:
+            print("  %-24s %5.1f%%  %7.0f cycles/chunk" % (nme, 100.0 * v[i] / tot, v[i] / max(rounds, 1)))
+    print("  total (parse waves)      %7.0f cycles/chunk" % (tot / max(rounds, 1)))
     itot = v[8] + v[9]
     for i, nme in enumerate(INAMES):
         print("  %-24s %5.1f%%  %7.0f cycles/round" % (nme, 100.0 * v[8 + i] / max(itot, 1), v[8 + i] / max(irounds, 1)))
