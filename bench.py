@@ -289,6 +289,14 @@ def main():
     extras = {}
     if args.extras:
         # validation (the decoder's walk + checks, no output) of the fast streams
+        # SM_MODE_FAST_DENSE: two chain candidates per position (smaller output, slower)
+        t_dc = time_kernel(lambda: batch.compress(sm, "dense"), 3)
+        extras["dense_compress_GBps"] = round(in_bytes / (t_dc * 1e-3) / 1e9, 3)
+        extras["dense_ratio"] = round(int(batch.comp_len.to(torch.int64).sum()) / in_bytes, 5)
+        t_dd = time_kernel(lambda: batch.uncompress(sm), 3)
+        ok = ok and batch.verify()
+        extras["dense_streams_uncompress_GBps"] = round(in_bytes / (t_dd * 1e-3) / 1e9, 3)
+        batch.compress(sm, "fast")
         vst = torch.full_like(batch.status, -1)
         t_v = time_kernel(lambda: sm.validate_batch_device(batch.d_comp, batch.comp_off, batch.comp_len, vst), 3)
         ok = ok and int(vst.abs().sum()) == 0

@@ -165,26 +165,40 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, typename C
   const uint32_t ngroups = min((n - r0 + 63) >> 6, kRP / 64);
   const bool full = r0 + kRP + 3 <= n;  // every position of the round has its 4 bytes
   const uint32_t sh = lane & 3u;
-  for (uint32_t g0 = 0; g0 < ngroups; g0 += kG) {
+  // software pipeline: the next step's words are read right behind this step's exchanges, so
+  // the two LDS round trips of a step overlap
+  uint32_t h[kG];
+  bool ok[kG];
+  auto hash_step = [&](uint32_t g0, uint32_t* hh, bool* oo) {
     const uint32_t base = r0 + 64 * g0;
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(data + base) + (lane >> 2);
-    uint32_t h[kG], old[kG];
-    bool ok[kG];
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
-      h[i] = fast_hash<kTabBits>(__builtin_amdgcn_alignbyte(dw[16 * i + 1], dw[16 * i], sh));
-      ok[i] = full || base + 64 * i + lane + 4 <= n;
+      hh[i] = fast_hash<kTabBits>(__builtin_amdgcn_alignbyte(dw[16 * i + 1], dw[16 * i], sh));
+      oo[i] = full || base + 64 * i + lane + 4 <= n;
     }
+  };
+  hash_step(0, h, ok);
+  for (uint32_t g0 = 0; g0 < ngroups; g0 += kG) {
+    const uint32_t base = r0 + 64 * g0;
+    uint32_t old[kG], hn[kG];
+    bool okn[kG];
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       old[i] = 0;
       if (ok[i]) old[i] = __hip_atomic_exchange(&T[h[i]], base + 64 * i + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    if (g0 + kG < ngroups) hash_step(g0 + kG, hn, okn);
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       // the old latest becomes the second-latest (the new entry's high half)
       if (D > 1 && ok[i]) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
       ring[64 * (g0 + i) + lane] = (typename Cfg<D>::Cand)old[i];
+    }
+#pragma unroll
+    for (int i = 0; i < kG; ++i) {
+      h[i] = hn[i];
+      ok[i] = okn[i];
     }
   }
 }
