@@ -5,6 +5,8 @@ export compress, uncompress
 
 const LIB = get(ENV, "SNAPPY_MI355X_LIB", "libsnappy_mi355x")
 const SM_MODE_REFERENCE = Cint(0)      # byte-identical to Snappy.jl
+const SM_MODE_FAST = Cint(1)           # wave-parallel parse; decodes bit-exactly under Snappy.jl
+const SM_MODE_FAST_DENSE = Cint(2)     # SM_MODE_FAST with two chain candidates: smaller output
 const CTX = Ref{Ptr{Cvoid}}(C_NULL)
 
 function __init__()
