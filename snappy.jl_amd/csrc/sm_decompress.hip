@@ -143,8 +143,14 @@ __device__ inline void ring_fill(const uint8_t* __restrict__ in, uint32_t N, uin
 // batch's own output (kLdsSrc + kBatchOut + margin <= kWin).  Bytes are written with aligned
 // ds_or_b64 pairs into bytes zeroed when the batch starts (a misaligned LDS write/read costs a
 // cycle per lane, tools/lds_bench.hip).
-constexpr uint32_t kWin = 4096;
-constexpr uint32_t kBatchOut = 1024;
+#ifndef SM_DEC_WIN
+#define SM_DEC_WIN 1024
+#endif
+constexpr uint32_t kWin = SM_DEC_WIN;
+#ifndef SM_DEC_BOUT
+#define SM_DEC_BOUT 512
+#endif
+constexpr uint32_t kBatchOut = SM_DEC_BOUT;
 constexpr uint32_t kLdsSrc = kWin - kBatchOut - 64;
 
 // 8 bytes at byte x of an LDS ring of msk+1 bytes (power of 2, 8-aligned base): two aligned
@@ -349,7 +355,9 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const uint32_t O0 = op;
       const uint32_t slo = opt - offset;
       const uint32_t shi = slo + min(len, offset);
-      const bool gsrc = !(SM_ABLATE_D & 4) && iscopy && offset > kLdsSrc;  // source older than the window: from HBM
+      // a source older than the window's reach comes from HBM -- if HBM already holds all of it
+      // (the last partial 16-byte block before the batch is only in the window)
+      const bool gsrc = !(SM_ABLATE_D & 4) && iscopy && offset > kLdsSrc && shi <= flushed;
       const uint64_t all = nt == 64 ? ~0ull : ((1ull << nt) - 1);
       const bool longlit = !iscopy && litlen > 64;
       uint64_t done = (ballot(longlit) & all) | ~all;
@@ -513,8 +521,10 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
       const uint32_t done16 = head + (n16 << 4);
       if (lane < litlen - done16) out[op + done16 + lane] = s[done16 + lane];
-      // the window keeps the literal's tail, which later copies may read
-      const uint32_t keep = min(litlen, kLdsSrc + 64);
+      // the window keeps the literal's tail, which later copies may read: every slot, since a
+      // copy that depends on the next batch's own output reads the window at offsets up to
+      // kBatchOut + 64 (more than kLdsSrc with a small window)
+      const uint32_t keep = min(litlen, kWin);
       const uint32_t t0 = op + litlen - keep;
       win_zero(win, t0, keep, lane);
       for (uint32_t x = 8 * lane; x < keep; x += 8 * kWave) {
@@ -568,7 +578,10 @@ __device__ inline int32_t parse_header(const uint8_t* in, uint32_t N, uint32_t l
   return st;
 }
 
-__global__ __launch_bounds__(64, 4) void k_decompress(DecompressArgs a) {
+#ifndef SM_DEC_OCC
+#define SM_DEC_OCC 7  // waves per SIMD: 72 VGPRs (2 spilled), 4.7 KB LDS per wave
+#endif
+__global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
   __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];  // tag-walk jump tables
   __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];                // output window

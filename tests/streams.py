@@ -52,8 +52,9 @@ def build(ops):
     return varint(len(out)) + bytes(body), bytes(out)
 
 
-def random_ops(rng, target, max_lit=300, max_off=65535, long_lit_p=0.02):
-    """Seeded mix of literals (some long) and copies (any legal offset, len 1..64)."""
+def random_ops(rng, target, max_lit=300, max_off=65535, long_lit_p=0.02, near=4096):
+    """Seeded mix of literals (some long) and copies (any legal offset, len 1..64); half of
+    the copies reach at most `near` bytes back."""
     ops, size = [], 0
     while size < target:
         if size == 0 or rng.random() < 0.3:
@@ -66,7 +67,7 @@ def random_ops(rng, target, max_lit=300, max_off=65535, long_lit_p=0.02):
             if r < 0.3:
                 off = int(rng.integers(1, min(size, 16) + 1))
             elif r < 0.8:
-                off = int(rng.integers(1, min(size, 4096) + 1))
+                off = int(rng.integers(1, min(size, near) + 1))
             else:
                 off = int(rng.integers(1, min(size, max_off) + 1))
             ln = int(rng.integers(1, 65))

@@ -265,15 +265,16 @@ def _decode_all(sm, streams):
 
 
 def test_decompress_window_boundaries(sm, oracle, gpu_available):
-    """Copies into long literals and across the LDS output window's reach (kLdsSrc = 3008:
-    nearer sources are read from LDS, farther ones from HBM), overlapping copies after a
-    long literal, and a batch whose output exceeds the 1 KiB batch cap."""
+    """Copies into long literals and across the LDS output window's reach (kLdsSrc =
+    kWin - kBatchOut - 64: 448 with the default 1 KiB window, 3008 with a 4 KiB one; nearer
+    sources are read from LDS, farther ones from HBM), overlapping copies after a long
+    literal, and batches whose output exceeds the batch cap."""
     from streams import build
     rng = np.random.default_rng(3)
     big = rng.integers(0, 256, 5000, dtype=np.uint8).tobytes()
     cases = []
-    for off in (1, 2, 7, 8, 15, 16, 17, 64, 100, 999, 2047, 2048, 3006, 3007, 3008, 3009, 3010, 4000, 4095,
-                4096, 4097, 4999, 5000):
+    for off in (1, 2, 7, 8, 15, 16, 17, 64, 100, 446, 447, 448, 449, 450, 511, 512, 513, 959, 960, 961, 999,
+                1023, 1024, 1025, 2047, 2048, 3006, 3007, 3008, 3009, 3010, 4000, 4095, 4096, 4097, 4999, 5000):
         for ln in (1, 4, 11, 12, 16, 33, 64):
             cases.append([("lit", big), ("copy", off, ln), ("copy", 3, 20), ("lit", b"xyz"), ("copy", off, ln)])
     mid = rng.integers(0, 256, 150, dtype=np.uint8).tobytes()  # a 65..200-byte literal
@@ -295,6 +296,9 @@ def test_decompress_random_op_streams(sm, gpu_available):
     from streams import build, random_ops
     rng = np.random.default_rng(2024)
     built = [build(random_ops(rng, int(rng.integers(1, 65536)))) for _ in range(400)]
+    # offsets around the decoder's LDS-window reach and batch cap (a source ending in the
+    # unflushed tail before a batch; a batch-dependent copy after a long literal)
+    built += [build(random_ops(rng, int(rng.integers(1, 65536)), long_lit_p=0.1, near=1200)) for _ in range(300)]
     outs = _decode_all(sm, [s for s, _ in built])
     for (s, expect), o in zip(built, outs):
         assert o == expect
