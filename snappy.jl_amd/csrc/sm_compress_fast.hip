@@ -175,7 +175,7 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, typename C
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       hh[i] = fast_hash<kTabBits>(__builtin_amdgcn_alignbyte(dw[16 * i + 1], dw[16 * i], sh));
-      oo[i] = full || base + 64 * i + lane + 4 <= n;
+      oo[i] = base + 64 * i + lane + 4 <= n;
     }
   };
   hash_step(0, h, ok);
@@ -186,13 +186,14 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, typename C
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       old[i] = 0;
-      if (ok[i]) old[i] = __hip_atomic_exchange(&T[h[i]], base + 64 * i + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (full || ok[i])
+        old[i] = __hip_atomic_exchange(&T[h[i]], base + 64 * i + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (g0 + kG < ngroups) hash_step(g0 + kG, hn, okn);
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       // the old latest becomes the second-latest (the new entry's high half)
-      if (D > 1 && ok[i]) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
+      if (D > 1 && (full || ok[i])) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
       ring[64 * (g0 + i) + lane] = (typename Cfg<D>::Cand)old[i];
     }
 #pragma unroll
@@ -410,9 +411,11 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   typedef typename C::Cand Cand;
   constexpr uint32_t kSlots = C::kSlots, kRP = C::kRoundPos;
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  uint8_t* data = smem;                                                     // 64 KiB block
-  uint32_t* T = reinterpret_cast<uint32_t*>(smem + kBlockSize);             // hash table
-  Cand* ring = reinterpret_cast<Cand*>(T + kTabBytes / 4);                  // 2 x kRoundPos candidates
+  // The table sits at LDS offset 0 (a bucket's address is h * 4) and the block right after it
+  // at 32 KiB, an offset the DS instructions' 16-bit immediate field carries for free.
+  uint32_t* T = reinterpret_cast<uint32_t*>(smem);                          // hash table
+  uint8_t* data = smem + kTabBytes;                                         // 64 KiB block
+  Cand* ring = reinterpret_cast<Cand*>(data + kBlockSize);                  // 2 x kRoundPos candidates
   uint32_t* csize = reinterpret_cast<uint32_t*>(ring + 2 * kRP);            // 2 x 32 chunk infos
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = uniform(tid >> 6);
