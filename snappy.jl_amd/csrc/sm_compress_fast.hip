@@ -30,6 +30,9 @@
 #ifndef SM_FAST_SHFL
 #define SM_FAST_SHFL 0
 #endif
+#ifndef SM_FAST_NMJ0
+#define SM_FAST_NMJ0 1  // J0 by a gather from a next-match row (0: per-position mask selects)
+#endif
 #ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches, 4 inserter only
 #define SM_ABLATE 0
 #endif
@@ -286,6 +289,29 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
 #pragma unroll
     for (int i = kP - 2; i >= 0; --i) F[i] = M[i + 1] ? 64u * (i + 1) + ctz64(M[i + 1]) : F[i + 1];
     uint32_t jv[kP];
+#if SM_FAST_NMJ0
+    // NM[x] = the first match position >= x, for this lane's positions (register j is word
+    // j of the masks, so no select); J0[r] = NM[r + L(r)]: NM goes to row 0, the match
+    // positions gather NM at r + L (all reads issued before the row is overwritten; entry
+    // kChunk holds kEnd) and store their J0.
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const uint32_t rr = 64 * j + lane;
+      const uint64_t m = M[j] >> lane;
+      jv[j] = m ? rr + ctz64(m) : F[j];
+      jt[rr] = (uint8_t)jv[j];
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    uint32_t g[kP];
+#pragma unroll
+    for (int j = 0; j < kP; ++j) g[j] = Ls[j] ? jt[64 * j + lane + Ls[j]] : jv[j];
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      jv[j] = g[j];
+      if (Ls[j]) jt[64 * j + lane] = (uint8_t)jv[j];
+    }
+#else
 #pragma unroll
     for (int j = 0; j < kP; ++j) {
       const uint32_t rr = 64 * j + lane;
@@ -301,6 +327,7 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
       jv[j] = m ? x + ctz64(m) : f;
       jt[rr] = (uint8_t)jv[j];
     }
+#endif
 #pragma unroll
     for (int kk = 1; kk < (int)kLevels; ++kk) {
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -459,6 +486,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     for (uint32_t k = tid; k < kTabBytes / 16; k += kThreads) t16[k] = z;  // 0 = no position
   }
   if (!inserter && kEnd == kChunk && lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
+  if (!inserter && lane == 0) jt[kChunk] = (uint8_t)kEnd;  // NM past the chunk: no match
   uint32_t op = 0;
   if (a.header) {
     uint32_t nb = varint_len(n);
