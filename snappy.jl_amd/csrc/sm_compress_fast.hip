@@ -432,17 +432,25 @@ __device__ inline void emit_chunk(uint8_t* dst, const uint8_t* data, const Chunk
   }
 }
 
+template <int D>
+constexpr size_t fast_lds() {
+  return kBlockSize + kTabBytes + Cfg<D>::kRingBytes + 4 * 64 + kPW * kLevels * kRow + kPW * 8 * kP;
+}
+static_assert(fast_lds<1>() <= 160 * 1024 && fast_lds<2>() <= 160 * 1024, "fast compressor LDS exceeds a CU");
+
 template <int kDepth>
 __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   typedef Cfg<kDepth> C;
   typedef typename C::Cand Cand;
   constexpr uint32_t kSlots = C::kSlots, kRP = C::kRoundPos;
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  // The table sits at LDS offset 0 (a bucket's address is h * 4) and the block right after it
-  // at 32 KiB, an offset the DS instructions' 16-bit immediate field carries for free.
-  uint32_t* T = reinterpret_cast<uint32_t*>(smem);                          // hash table
-  uint8_t* data = smem + kTabBytes;                                         // 64 KiB block
-  Cand* ring = reinterpret_cast<Cand*>(data + kBlockSize);                  // 2 x kRoundPos candidates
+  // static LDS: every address is a link-time constant (a dynamic allocation's base costs a
+  // v_add of its relocated 0 on every access)
+  __shared__ __attribute__((aligned(16))) uint8_t smem[fast_lds<kDepth>()];
+  // The block sits at LDS offset 0, so a chain candidate (a position) is its own byte address;
+  // the table follows it (a bucket's address is one v_lshl_add).
+  uint8_t* data = smem;                                                     // 64 KiB block
+  uint32_t* T = reinterpret_cast<uint32_t*>(smem + kBlockSize);             // hash table
+  Cand* ring = reinterpret_cast<Cand*>(smem + kBlockSize + kTabBytes);      // 2 x kRoundPos candidates
   uint32_t* csize = reinterpret_cast<uint32_t*>(ring + 2 * kRP);            // 2 x 32 chunk infos
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = uniform(tid >> 6);
@@ -630,22 +638,11 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 }
 #endif
 
-template <int D>
-constexpr size_t fast_lds() {
-  return kBlockSize + kTabBytes + Cfg<D>::kRingBytes + 4 * 64 + kPW * kLevels * kRow + kPW * 8 * kP;
-}
-static_assert(fast_lds<1>() <= 160 * 1024 && fast_lds<2>() <= 160 * 1024, "fast compressor LDS exceeds a CU");
+
 
 template <int D>
 static hipError_t launch_depth(const CompressArgs& a, hipStream_t s) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_compress_fast<D>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)fast_lds<D>());
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(k_compress_fast<D>, dim3(a.nblk), dim3(kThreads), fast_lds<D>(), s, a);
+  hipLaunchKernelGGL(k_compress_fast<D>, dim3(a.nblk), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
