@@ -400,7 +400,9 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
               const uint32_t msk = iscopy ? kWin - 1 : kRing - 1;
               const uint32_t sp = iscopy ? slo : lsrc;
               const uint32_t off = iscopy ? offset : 0xffffu;
-              const uint64_t B = gsrc ? *reinterpret_cast<const du64u*>(out + slo) : lds_get8w(bb, msk, sp);
+              // S's first 8 bytes, needed only when S wraps inside this pass (offset < base + 16)
+              uint64_t B = 0;
+              if (off < base + 8 * kPass) B = gsrc ? *reinterpret_cast<const du64u*>(out + slo) : lds_get8w(bb, msk, sp);
               uint32_t m0 = base;
               while (m0 >= off) m0 -= off;
               uint32_t m = m0;
