@@ -10,3 +10,34 @@ def test_swar_tag_sizes_equal_per_byte_definition(tmp_path):
     subprocess.run(["gcc", "-O2", "-o", str(exe), os.path.join(ROOT, "tools", "check_tag_sizes.c")], check=True)
     out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
     assert out.startswith("bad 0,"), out
+
+
+def test_kernel_register_budgets(tmp_path):
+    """gfx950 resource usage of the hot kernels (hipcc -Rpass-analysis, no GPU needed):
+    no VGPR spills in the fast compressor, and below the 128-VGPR ceiling that 16-wave
+    workgroups allow -- a build of the two-chunk parse that landed exactly on 128 produced
+    invalid streams; the decoder keeps 7 waves per SIMD."""
+    import re
+    csrc = os.path.join(ROOT, "snappy.jl_amd", "csrc")
+    usage = {}
+    for src in ("sm_compress_fast.hip", "sm_decompress.hip"):
+        out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-strict-aliasing",
+                              "-fPIC", "-Rpass-analysis=kernel-resource-usage", "--cuda-device-only", "-c",
+                              os.path.join(csrc, src), "-o", str(tmp_path / (src + ".o"))],
+                             capture_output=True, text=True, check=True).stderr
+        name = None
+        for line in out.splitlines():
+            m = re.search(r"Function Name: (\S+)", line)
+            if m:
+                name = m.group(1)
+                usage[name] = {}
+                continue
+            m = re.search(r"remark:\s+(VGPRs|VGPRs Spill|Occupancy \[waves/SIMD\]): (\d+)", line)
+            if m and name:
+                usage[name][m.group(1)] = int(m.group(2))
+    fast = [k for k in usage if "k_compress_fast" in k]
+    assert len(fast) == 2, usage.keys()
+    for k in fast:
+        assert usage[k]["VGPRs"] < 128 and usage[k]["VGPRs Spill"] == 0, (k, usage[k])
+    dec = [k for k in usage if k.endswith("k_decompressENS_14DecompressArgsE")]
+    assert dec and usage[dec[0]]["Occupancy [waves/SIMD]"] >= 7, usage.get(dec[0] if dec else None)
