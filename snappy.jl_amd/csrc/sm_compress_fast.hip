@@ -30,10 +30,13 @@
 #ifndef SM_FAST_SHFL
 #define SM_FAST_SHFL 0
 #endif
+#ifndef SM_FAST_EXT16
+#define SM_FAST_EXT16 1  // match extension 16 bytes per step (0: 8)
+#endif
 #ifndef SM_FAST_NMJ0
 #define SM_FAST_NMJ0 1  // J0 by a gather from a next-match row (0: per-position mask selects)
 #endif
-#ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches, 4 inserter only
+#ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches, 4 inserter only, 8 no extension past 8 bytes
 #define SM_ABLATE 0
 #endif
 
@@ -257,14 +260,31 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
   for (int j = 0; j < kP; ++j) {
     const uint32_t q = c0 + 64 * j + lane;
     uint32_t L = Ls[j];
-    bool more = L >= 8 && q + L < ce;
+    bool more = !(SM_ABLATE & 8) && L >= 8 && q + L < ce;
     while (ballot(more)) {
       if (more) {
+#if SM_FAST_EXT16
+        // 16 bytes per step: five aligned dwords per side, four funnel shifts each
+        const uint32_t avail = ce - q - L;
+        const uint32_t a = q - offs[j] + L, b = q + L;
+        const uint32_t* wa = reinterpret_cast<const uint32_t*>(data + (a & ~3u));
+        const uint32_t* wb = reinterpret_cast<const uint32_t*>(data + (b & ~3u));
+        const uint32_t sa = a & 3u, sb = b & 3u;
+        uint32_t x[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          x[k] = __builtin_amdgcn_alignbyte(wa[k + 1], wa[k], sa) ^ __builtin_amdgcn_alignbyte(wb[k + 1], wb[k], sb);
+        const uint64_t lo = ((uint64_t)x[1] << 32) | x[0], hi = ((uint64_t)x[3] << 32) | x[2];
+        const uint32_t fb = lo ? (uint32_t)(__builtin_ctzll(lo) >> 3) : (hi ? 8u + (uint32_t)(__builtin_ctzll(hi) >> 3) : 16u);
+        L += min(fb, avail);
+        more = fb == 16 && avail > 16;
+#else
         const uint32_t avail = ce - q - L;
         const uint64_t x = lds_ld64(data, q - offs[j] + L) ^ lds_ld64(data, q + L);
         const uint32_t fb = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
         L += min(fb, avail);
         more = fb == 8 && avail > 8;
+#endif
       }
     }
     Ls[j] = (SM_ABLATE & 2) ? 0u : L;
