@@ -27,15 +27,6 @@
 #include "sm_device.h"
 #include "sm_internal.h"
 
-#ifndef SM_FAST_SHFL
-#define SM_FAST_SHFL 0
-#endif
-#ifndef SM_FAST_EXT16
-#define SM_FAST_EXT16 1  // match extension 16 bytes per step (0: 8)
-#endif
-#ifndef SM_FAST_NMJ0
-#define SM_FAST_NMJ0 1  // J0 by a gather from a next-match row (0: per-position mask selects)
-#endif
 #ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches, 4 inserter only, 8 no extension past 8 bytes
 #define SM_ABLATE 0
 #endif
@@ -255,7 +246,7 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
     Ls[j] = min(L, ce - q);
     offs[j] = q - c;
   }
-  // finish matches that filled the 8-byte window: 8 bytes per lane per step
+  // finish matches that filled the 8-byte window: 16 bytes per lane per step
 #pragma unroll
   for (int j = 0; j < kP; ++j) {
     const uint32_t q = c0 + 64 * j + lane;
@@ -263,7 +254,6 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
     bool more = !(SM_ABLATE & 8) && L >= 8 && q + L < ce;
     while (ballot(more)) {
       if (more) {
-#if SM_FAST_EXT16
         // 16 bytes per step: five aligned dwords per side, four funnel shifts each
         const uint32_t avail = ce - q - L;
         const uint32_t a = q - offs[j] + L, b = q + L;
@@ -278,13 +268,6 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
         const uint32_t fb = lo ? (uint32_t)(__builtin_ctzll(lo) >> 3) : (hi ? 8u + (uint32_t)(__builtin_ctzll(hi) >> 3) : 16u);
         L += min(fb, avail);
         more = fb == 16 && avail > 16;
-#else
-        const uint32_t avail = ce - q - L;
-        const uint64_t x = lds_ld64(data, q - offs[j] + L) ^ lds_ld64(data, q + L);
-        const uint32_t fb = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
-        L += min(fb, avail);
-        more = fb == 8 && avail > 8;
-#endif
       }
     }
     Ls[j] = (SM_ABLATE & 2) ? 0u : L;
@@ -309,7 +292,6 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
 #pragma unroll
     for (int i = kP - 2; i >= 0; --i) F[i] = M[i + 1] ? 64u * (i + 1) + ctz64(M[i + 1]) : F[i + 1];
     uint32_t jv[kP];
-#if SM_FAST_NMJ0
     // NM[x] = the first match position >= x, for this lane's positions (register j is word
     // j of the masks, so no select); J0[r] = NM[r + L(r)]: NM goes to row 0, the match
     // positions gather NM at r + L (all reads issued before the row is overwritten; entry
@@ -331,23 +313,6 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
       jv[j] = g[j];
       if (Ls[j]) jt[64 * j + lane] = (uint8_t)jv[j];
     }
-#else
-#pragma unroll
-    for (int j = 0; j < kP; ++j) {
-      const uint32_t rr = 64 * j + lane;
-      const uint32_t x = rr + Ls[j];  // <= kChunk: copies end inside the chunk
-      const uint32_t i = x >> 6;
-      uint64_t mw = M[0];
-#pragma unroll
-      for (int u = 1; u < kP; ++u) mw = i == (uint32_t)u ? M[u] : mw;
-      uint32_t f = kEnd;
-#pragma unroll
-      for (int u = 0; u < kP; ++u) f = i == (uint32_t)u ? F[u] : f;
-      const uint64_t m = i < (uint32_t)kP ? mw >> (x & 63u) : 0;
-      jv[j] = m ? x + ctz64(m) : f;
-      jt[rr] = (uint8_t)jv[j];
-    }
-#endif
 #pragma unroll
     for (int kk = 1; kk < (int)kLevels; ++kk) {
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -579,19 +544,11 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       const uint32_t info = lane < kSlots ? cinfo[lane] : 0u;
       const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0x1ffu, trl = (info >> 20) & 0x1ffu;
       const bool nocp = (info >> 29) & 1u;
-#if SM_FAST_SHFL
-      const uint32_t trl_prev = lane ? __shfl_up(trl, 1, 64) : 0u;
-#else
       const uint32_t trl_prev = __builtin_amdgcn_update_dpp(0u, trl, 0x138, 0xf, 0xf, false);  // wave_shr:1
-#endif
       const bool cont_in = lane > 0 && lane < kSlots && trl_prev > 0 && lead > 0;
       const bool mid = nocp && cont_in;
       const bool start = trl > 0 && !mid;
-#if SM_FAST_SHFL
-      const bool cont_next = __shfl_down((uint32_t)cont_in, 1, 64) != 0 && lane < 63;
-#else
       const bool cont_next = __builtin_amdgcn_update_dpp(0u, (uint32_t)cont_in, 0x130, 0xf, 0xf, false) != 0;  // wave_shl:1
-#endif
       const uint32_t cu = (r * kSlots + lane) * kChunk;                      // chunk start
       const uint32_t ceu = min(cu + kChunk, n);
       // the run ending in chunk u ends at cu + lead; a run starting in chunk v ends in the
@@ -610,11 +567,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
           nxt = (lane + d < kSlots && o2 < nxt) ? o2 : nxt;
         }
       }
-#if SM_FAST_SHFL
-      nxt = lane < 63 ? __shfl_down(nxt, 1, 64) : 0xffu;
-#else
       nxt = __builtin_amdgcn_update_dpp(0xffu, nxt, 0x130, 0xf, 0xf, false);                       // first end after u
-#endif
       const uint32_t endpos = __shfl(cu + lead, nxt & 63u, 64);
       const uint32_t runlen = (start && cont_next) ? endpos - (ceu - trl) : 0u;
       const uint32_t Sm = S - (cont_in ? lit_tag_bytes(lead) : 0u) +
