@@ -56,7 +56,10 @@ constexpr uint32_t kMaxBatchLit = 200;  // longer literals stop a window walk (s
 constexpr int kWalkLevels = 5;  // tables J0..J4 in LDS; J5 (bit 5 of a lane's chain index) = J4 o J4
 constexpr int kJtRow = 264;             // a jump-table row (u16): positions 0..255, then 256 = beyond the window
 constexpr int kJt = kWalkLevels * kJtRow;  // u16 jump-table entries of a walk
-constexpr int kPass = 2;        // 8-byte chunks per execution pass (most tags are <= 16 B)
+#ifndef SM_DEC_PASS
+#define SM_DEC_PASS 2
+#endif
+constexpr int kPass = SM_DEC_PASS;  // 8-byte chunks per execution pass (most tags are <= 16 B)
 
 __device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
   if (p + 3 < N && (((uintptr_t)(in + p)) & 3) == 0) return *reinterpret_cast<const uint32_t*>(in + p);
