@@ -411,16 +411,25 @@ __device__ inline void emit_chunk(uint8_t* dst, const uint8_t* data, const Chunk
   }
   const uint32_t delta = o + mytag - t.ls;  // output - input position of the run (mod 2^32)
   const uint32_t end = tq + tL;
-  uint32_t below = 0;
+  // all LDS reads (the literal bytes, the shuffles) of the four position groups are issued
+  // before the first store, so their round trips overlap
+  uint32_t below = 0, cnt[kP], pend[kP], dl[kP], v[kP];
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    v[j] = data[t.c0 + 64 * j + lane];  // inside the block area even past ce (not stored then)
+    cnt[j] = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(t.ts[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)t.ts[j], 0u));
+    cnt[j] += (uint32_t)(t.ts[j] >> lane) & 1u;  // tokens whose copy starts at or before x
+    below += __builtin_popcountll(t.ts[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    pend[j] = __shfl(end, cnt[j] ? cnt[j] - 1 : 0, 64);
+    dl[j] = __shfl(delta, cnt[j], 64);
+  }
 #pragma unroll
   for (int j = 0; j < kP; ++j) {
     const uint32_t x = t.c0 + 64 * j + lane;
-    uint32_t cnt = below + __builtin_amdgcn_mbcnt_hi((uint32_t)(t.ts[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)t.ts[j], 0u));
-    cnt += (uint32_t)(t.ts[j] >> lane) & 1u;  // tokens whose copy starts at or before x
-    const uint32_t pend = __shfl(end, cnt ? cnt - 1 : 0, 64);
-    const uint32_t dl = __shfl(delta, cnt, 64);
-    if (x < t.ce && (cnt == 0 || x >= pend)) dst[x + dl] = data[x];  // 32-bit offset: saddr store
-    below += __builtin_popcountll(t.ts[j]);
+    if (x < t.ce && (cnt[j] == 0 || x >= pend[j])) dst[x + dl[j]] = (uint8_t)v[j];  // 32-bit offset: saddr store
   }
 }
 
