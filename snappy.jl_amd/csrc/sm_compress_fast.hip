@@ -62,6 +62,9 @@ constexpr uint32_t kLevels = kChunk == 256 ? 6 : 5;
 // names it and it maps to itself at every level
 constexpr uint32_t kEnd = kChunk == 256 ? 255 : kChunk;
 constexpr uint32_t kRow = kChunk + 8;         // a jump-table row (8-B aligned)
+// levels built: for 256-byte chunks J0..J4 (16 steps); a chain longer than 32 elements
+// (element 31 is a copy) finishes with two more J4 steps instead of a J5 level
+constexpr uint32_t kBuilt = kChunk == 256 ? kLevels - 1 : kLevels;
 
 // literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
 __device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
@@ -321,7 +324,7 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
       if (Ls[j]) jt[64 * j + lane] = (uint8_t)jv[j];
     }
 #pragma unroll
-    for (int kk = 1; kk < (int)kLevels; ++kk) {
+    for (int kk = 1; kk < (int)kBuilt; ++kk) {
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
 #pragma unroll
       for (int j = 0; j < kP; ++j) {
@@ -335,9 +338,21 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
     // copies; past the last copy the chain sits at kEnd (no match).
     uint32_t c = 0;
 #pragma unroll
-    for (int kk = 0; kk < (int)kLevels; ++kk) {
+    for (int kk = 0; kk < (int)kBuilt; ++kk) {
       const uint32_t tt = jt[kk * kRow + c];
       c = ((lane >> kk) & 1u) ? tt : c;
+    }
+    if (kBuilt < kLevels) {
+      // lane t >= 32 holds element t - 32: element t is kEnd when element 31 is, else (a
+      // chain of more than 32 elements, rare) 32 steps further, two applications of J4
+      if (readlane(c, 31) < kEnd) {
+        if (lane >= 32) {
+          c = jt[(kBuilt - 1) * kRow + c];
+          c = jt[(kBuilt - 1) * kRow + c];
+        }
+      } else {
+        c = lane >= 32 ? kEnd : c;
+      }
     }
     // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles of
     // length | offset << 9
