@@ -63,8 +63,12 @@ constexpr uint32_t kLevels = kChunk == 256 ? 6 : 5;
 constexpr uint32_t kEnd = kChunk == 256 ? 255 : kChunk;
 constexpr uint32_t kRow = kChunk + 8;         // a jump-table row (8-B aligned)
 // levels built: for 256-byte chunks J0..J4 (16 steps); a chain longer than 32 elements
-// (element 31 is a copy) finishes with two more J4 steps instead of a J5 level
-constexpr uint32_t kBuilt = kChunk == 256 ? kLevels - 1 : kLevels;
+// (element 31 is a copy) finishes with two more J4 steps instead of a J5 level (4.15 ->
+// 4.11 ms on the bench text; building J0..J3 or J0..J2 and stepping more: within noise)
+#ifndef SM_FAST_BUILT
+#define SM_FAST_BUILT 5
+#endif
+constexpr uint32_t kBuilt = kChunk == 256 ? SM_FAST_BUILT : kLevels;
 
 // literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
 __device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
@@ -342,16 +346,19 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
       const uint32_t tt = jt[kk * kRow + c];
       c = ((lane >> kk) & 1u) ? tt : c;
     }
-    if (kBuilt < kLevels) {
-      // lane t >= 32 holds element t - 32: element t is kEnd when element 31 is, else (a
-      // chain of more than 32 elements, rare) 32 steps further, two applications of J4
-      if (readlane(c, 31) < kEnd) {
-        if (lane >= 32) {
+    // lane t >= S = 2^kBuilt holds element t mod S: the lanes >= kS advance S steps (two
+    // applications of the last level) while element kS - 1 is a copy, else they are past
+    // the chain's end
+#pragma unroll
+    for (uint32_t kS = 1u << kBuilt; kS < 64; kS += 1u << kBuilt) {
+      if (readlane(c, kS - 1) < kEnd) {
+        if (lane >= kS) {
           c = jt[(kBuilt - 1) * kRow + c];
           c = jt[(kBuilt - 1) * kRow + c];
         }
       } else {
-        c = lane >= 32 ? kEnd : c;
+        c = lane >= kS ? kEnd : c;
+        break;
       }
     }
     // the match at c is held by lane c mod 64 (register c / 64): full-wave shuffles of
