@@ -139,6 +139,18 @@ sm_status sm_uncompress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in
                               uint32_t nblk, uint8_t* out, const uint64_t* out_off, const uint32_t* out_cap,
                               uint32_t* out_len, int32_t* status);
 
+/* Multi-GPU, one process: the blocks are cut into nctx contiguous shards of (nearly) equal
+ * block count, shard i runs sm_compress_batch / sm_uncompress_batch on ctxs[i] (one context per
+ * GPU) from its own host thread, all shards concurrently.  Same arguments and per-block results
+ * as the single-context calls; the first failing shard's status is returned.  The
+ * one-process-per-GPU path (torch.distributed, snappy.jl_amd/dist.py) is the alternative. */
+sm_status sm_compress_batch_sharded(sm_ctx* const* ctxs, int nctx, const uint8_t* in, const uint64_t* in_off,
+                                    const uint32_t* in_len, uint32_t nblk, uint8_t* out, const uint64_t* out_off,
+                                    uint32_t* out_len, int mode);
+sm_status sm_uncompress_batch_sharded(sm_ctx* const* ctxs, int nctx, const uint8_t* in, const uint64_t* in_off,
+                                      const uint32_t* in_len, uint32_t nblk, uint8_t* out, const uint64_t* out_off,
+                                      const uint32_t* out_cap, uint32_t* out_len, int32_t* status);
+
 /* snappy_validate_compressed_buffer (snappy-c.h) for one host buffer, on the device: the status
  * sm_uncompress would return with enough output room, without decoding into memory. */
 sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, size_t compressed_length);

@@ -41,7 +41,7 @@ ABI_SYMBOLS = (
     "sm_compress_batch_device", "sm_uncompress_batch_device", "sm_compress_batch",
     "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device", "sm_ctx_last_path",
     "sm_find_match_length", "sm_validate_batch_device", "sm_uncompressed_length_batch_device",
-    "sm_validate_compressed_buffer",
+    "sm_validate_compressed_buffer", "sm_compress_batch_sharded", "sm_uncompress_batch_sharded",
 )
 
 
@@ -97,6 +97,10 @@ def lib():
         L.sm_compress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
         L.sm_uncompress_batch.restype = i32
         L.sm_uncompress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+        L.sm_compress_batch_sharded.restype = i32
+        L.sm_compress_batch_sharded.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
+        L.sm_uncompress_batch_sharded.restype = i32
+        L.sm_uncompress_batch_sharded.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp, vp, vp, vp]
         L.sm_find_match_length.restype = i32
         L.sm_find_match_length.argtypes = [vp, sz, sz, sz, sz, ctypes.POINTER(sz)]
         L.sm_ctx_last_path.restype = ctypes.c_int
@@ -137,6 +141,24 @@ def context(device=0):
             raise SnappyError(32, "no usable HIP device %d for snappy_mi355x" % device)
         _ctx[device] = c
     return c
+
+
+def contexts(devices):
+    """One sm_ctx per entry of `devices` for the sharded calls; a device listed twice gets a
+    second context (its own stream), so the sharding also runs on one GPU."""
+    seen, out = {}, []
+    for d in devices:
+        k = seen.get(d, 0)
+        seen[d] = k + 1
+        key = d if k == 0 else (d, k)
+        c = _ctx.get(key)
+        if c is None:
+            c = lib().sm_ctx_create(d)
+            if not c:
+                raise SnappyError(32, "no usable HIP device %d for snappy_mi355x" % d)
+            _ctx[key] = c
+        out.append(c)
+    return (ctypes.c_void_p * len(out))(*out)
 
 
 def _mode(mode):
@@ -239,8 +261,9 @@ def slot_offsets(in_len):
     return offs, caps
 
 
-def compress_batch(blocks, mode="fast", device=0):
-    """Compress independent <=64 KiB blocks; returns a list of snappy streams (bytes)."""
+def compress_batch(blocks, mode="fast", device=0, devices=None):
+    """Compress independent <=64 KiB blocks; returns a list of snappy streams (bytes).
+    devices: a list of GPUs to shard the blocks over from this one process."""
     buf, in_off, in_len = pack_blocks(blocks)
     if np.any(in_len > BLOCK_SIZE):
         raise ValueError("batch blocks must be <= 65536 bytes")
@@ -249,16 +272,20 @@ def compress_batch(blocks, mode="fast", device=0):
     out_len = np.zeros(len(blocks), dtype=np.uint32)
     if not blocks:
         return []
-    st = lib().sm_compress_batch(context(device), buf.ctypes.data, in_off.ctypes.data, in_len.ctypes.data,
-                                 len(blocks), out.ctypes.data, out_off.ctypes.data, out_len.ctypes.data,
-                                 _mode(mode))
+    args = (buf.ctypes.data, in_off.ctypes.data, in_len.ctypes.data, len(blocks), out.ctypes.data,
+            out_off.ctypes.data, out_len.ctypes.data, _mode(mode))
+    if devices is None:
+        st = lib().sm_compress_batch(context(device), *args)
+    else:  # one shard of the blocks per device, concurrently (sm_compress_batch_sharded)
+        st = lib().sm_compress_batch_sharded(contexts(devices), len(devices), *args)
     if st:
         raise SnappyError(st)
     return [out[int(o): int(o) + int(l)].tobytes() for o, l in zip(out_off, out_len)]
 
 
-def uncompress_batch(streams, capacities=None, device=0):
-    """Decode independent snappy streams; returns (list of bytes-or-None, status array)."""
+def uncompress_batch(streams, capacities=None, device=0, devices=None):
+    """Decode independent snappy streams; returns (list of bytes-or-None, status array).
+    devices: as in compress_batch."""
     if not streams:
         return [], np.zeros(0, np.int32)
     buf, in_off, in_len = pack_blocks(streams)
@@ -277,9 +304,12 @@ def uncompress_batch(streams, capacities=None, device=0):
     out = np.empty(max(int(cap.astype(np.uint64).sum()), 1), dtype=np.uint8)
     out_len = np.zeros(len(streams), dtype=np.uint32)
     status = np.zeros(len(streams), dtype=np.int32)
-    st = lib().sm_uncompress_batch(context(device), buf.ctypes.data, in_off.ctypes.data, in_len.ctypes.data,
-                                   len(streams), out.ctypes.data, out_off.ctypes.data, cap.ctypes.data,
-                                   out_len.ctypes.data, status.ctypes.data)
+    args = (buf.ctypes.data, in_off.ctypes.data, in_len.ctypes.data, len(streams), out.ctypes.data,
+            out_off.ctypes.data, cap.ctypes.data, out_len.ctypes.data, status.ctypes.data)
+    if devices is None:
+        st = lib().sm_uncompress_batch(context(device), *args)
+    else:
+        st = lib().sm_uncompress_batch_sharded(contexts(devices), len(devices), *args)
     if st:
         raise SnappyError(st)
     res = [out[int(o): int(o) + int(l)].tobytes() if s == 0 else None for o, l, s in zip(out_off, out_len, status)]

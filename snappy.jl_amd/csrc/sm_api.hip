@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/snappy_mi355x.h"
@@ -160,6 +161,54 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   do {                              \
     if ((x) != hipSuccess) return SM_ERR_DEVICE; \
   } while (0)
+
+namespace {
+// Shard [b0, b1) of a host batch, rebased so the single-context call copies only the shard's
+// bytes: offsets relative to the shard's lowest input / output offset.
+struct Shard {
+  uint32_t b0 = 0, n = 0;
+  uint64_t in_base = 0, out_base = 0;
+  std::vector<uint64_t> in_off, out_off;
+};
+
+std::vector<Shard> make_shards(int nctx, uint32_t nblk, const uint64_t* in_off, const uint64_t* out_off) {
+  std::vector<Shard> sh((size_t)nctx);
+  for (int i = 0; i < nctx; ++i) {
+    Shard& s = sh[(size_t)i];
+    s.b0 = (uint32_t)((uint64_t)nblk * (uint64_t)i / (uint64_t)nctx);
+    s.n = (uint32_t)((uint64_t)nblk * (uint64_t)(i + 1) / (uint64_t)nctx) - s.b0;
+    if (s.n == 0) continue;
+    s.in_base = *std::min_element(in_off + s.b0, in_off + s.b0 + s.n);
+    s.out_base = *std::min_element(out_off + s.b0, out_off + s.b0 + s.n);
+    s.in_off.resize(s.n);
+    s.out_off.resize(s.n);
+    for (uint32_t k = 0; k < s.n; ++k) {
+      s.in_off[k] = in_off[s.b0 + k] - s.in_base;
+      s.out_off[k] = out_off[s.b0 + k] - s.out_base;
+    }
+  }
+  return sh;
+}
+
+template <typename F>
+sm_status run_shards(int nctx, F&& shard_fn) {
+  std::vector<sm_status> st((size_t)nctx, SM_OK);
+  std::vector<std::thread> th;
+  th.reserve((size_t)nctx);
+  for (int i = 0; i < nctx; ++i) th.emplace_back([&, i] { st[(size_t)i] = shard_fn(i); });
+  for (auto& t : th) t.join();
+  for (sm_status x : st)
+    if (x != SM_OK) return x;
+  return SM_OK;
+}
+
+bool valid_ctxs(sm_ctx* const* ctxs, int nctx) {
+  if (!ctxs || nctx <= 0) return false;
+  for (int i = 0; i < nctx; ++i)
+    if (!ctxs[i]) return false;
+  return true;
+}
+}  // namespace
 
 extern "C" {
 
@@ -434,6 +483,38 @@ sm_status sm_uncompressed_length_batch_device(sm_ctx* ctx, const uint8_t* d_in, 
   DeviceGuard g(ctx->device);
   SM_CHECK(sm::launch_uncompressed_length(d_in, d_in_off, d_in_len, nblk, d_len, d_status, (hipStream_t)stream));
   return SM_OK;
+}
+
+sm_status sm_compress_batch_sharded(sm_ctx* const* ctxs, int nctx, const uint8_t* in, const uint64_t* in_off,
+                                    const uint32_t* in_len, uint32_t nblk, uint8_t* out, const uint64_t* out_off,
+                                    uint32_t* out_len, int mode) {
+  if (!valid_ctxs(ctxs, nctx) || !valid_mode(mode)) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!in || !in_off || !in_len || !out || !out_off || !out_len) return SM_ERR_ARGUMENT;
+  for (uint32_t b = 0; b < nblk; ++b)
+    if (in_len[b] > SM_BLOCK_SIZE) return SM_ERR_ARGUMENT;
+  const std::vector<Shard> sh = make_shards(nctx, nblk, in_off, out_off);
+  return run_shards(nctx, [&](int i) -> sm_status {
+    const Shard& s = sh[(size_t)i];
+    if (s.n == 0) return SM_OK;
+    return sm_compress_batch(ctxs[i], in + s.in_base, s.in_off.data(), in_len + s.b0, s.n, out + s.out_base,
+                             s.out_off.data(), out_len + s.b0, mode);
+  });
+}
+
+sm_status sm_uncompress_batch_sharded(sm_ctx* const* ctxs, int nctx, const uint8_t* in, const uint64_t* in_off,
+                                      const uint32_t* in_len, uint32_t nblk, uint8_t* out, const uint64_t* out_off,
+                                      const uint32_t* out_cap, uint32_t* out_len, int32_t* status) {
+  if (!valid_ctxs(ctxs, nctx)) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!in || !in_off || !in_len || !out || !out_off || !out_cap || !out_len || !status) return SM_ERR_ARGUMENT;
+  const std::vector<Shard> sh = make_shards(nctx, nblk, in_off, out_off);
+  return run_shards(nctx, [&](int i) -> sm_status {
+    const Shard& s = sh[(size_t)i];
+    if (s.n == 0) return SM_OK;
+    return sm_uncompress_batch(ctxs[i], in + s.in_base, s.in_off.data(), in_len + s.b0, s.n, out + s.out_base,
+                               s.out_off.data(), out_cap + s.b0, out_len + s.b0, status + s.b0);
+  });
 }
 
 sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, size_t n) {

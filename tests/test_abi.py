@@ -109,3 +109,14 @@ def test_mode_names_match_header(sm):
                         "dense": enum["SM_MODE_FAST_DENSE"]}
     with pytest.raises(ValueError):
         sm._mode("turbo")
+
+
+def test_sharded_calls_reject_bad_contexts(sm):
+    # argument checks happen on the host before any device work
+    L = sm.lib()
+    z = ctypes.c_void_p(0)
+    none = (ctypes.c_void_p * 1)(None)
+    assert L.sm_compress_batch_sharded(none, 1, z, z, z, 1, z, z, z, 1) == 33
+    assert L.sm_compress_batch_sharded(None, 0, z, z, z, 1, z, z, z, 1) == 33
+    assert L.sm_uncompress_batch_sharded(none, 1, z, z, z, 1, z, z, z, z, z) == 33
+    assert L.sm_uncompress_batch_sharded(None, -1, z, z, z, 1, z, z, z, z, z) == 33

@@ -175,6 +175,30 @@ def test_decompress_batched_blocks(sm, oracle, gpu_available, corpus):
         assert o == oracle.uncompress(s)
 
 
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_sharded_host_batches(sm, oracle, gpu_available, corpus, ndev):
+    # sm_{,un}compress_batch_sharded: one context per shard (all on device 0 here), shards
+    # rebased and run from concurrent host threads; results equal the single-context calls
+    blocks = []
+    for raw in corpus.values():
+        blocks.extend(blocks_of(raw))
+    blocks += [b"", b"a", bytes(range(256)) * 7]
+    devs = [0] * ndev
+    for mode in ("reference", "fast"):
+        outs = sm.compress_batch(blocks, mode=mode, devices=devs)
+        assert outs == sm.compress_batch(blocks, mode=mode)
+        if mode == "reference":
+            assert outs == [oracle.compress(b) for b in blocks]
+    streams = [oracle.compress(b) for b in blocks]
+    streams[5] = streams[5][:-3]  # a truncated stream: its own status, the rest decode
+    dec, status = sm.uncompress_batch(streams, devices=devs)
+    ref_dec, ref_status = sm.uncompress_batch(streams)
+    assert list(status) == list(ref_status) and status[5] != 0 and not np.delete(status, 5).any()
+    assert dec == ref_dec
+    for i, (b, d) in enumerate(zip(blocks, dec)):
+        assert d == (None if i == 5 else b)
+
+
 def _status(sm, data):
     try:
         return 0, sm.uncompress(data)
