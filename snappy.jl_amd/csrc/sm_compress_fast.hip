@@ -70,6 +70,15 @@ constexpr uint32_t kRow = kChunk + 8;         // a jump-table row (8-B aligned)
 #endif
 constexpr uint32_t kBuilt = kChunk == 256 ? SM_FAST_BUILT : kLevels;
 
+// Longest copy the parse takes (0: to the chunk end).  64 is emit_copy!'s own piece size, so a
+// longer match costs the same bytes as 64-byte copies chained through the next positions'
+// candidates; capping bounds the extension loop at four steps (text: 4.13 -> 4.09 ms, ratio
+// 0.5977 -> 0.5978; 128 gains nothing).
+#ifndef SM_FAST_LCAP
+#define SM_FAST_LCAP 64
+#endif
+constexpr bool kShortCopies = SM_FAST_LCAP != 0 && SM_FAST_LCAP <= 64;  // one piece per copy
+
 // literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
 __device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
 
@@ -86,6 +95,7 @@ __device__ inline void put_lit_tag(uint8_t* dst, uint32_t o, uint32_t ts, uint32
 
 // emit_copy! byte count (internal.jl:306-329), closed form
 __device__ inline uint32_t copy_bytes_cf(uint32_t off, uint32_t L) {
+  if (kShortCopies) return (L < 12 && off < 2048) ? 2 : 3;
   uint32_t k = L >= 68 ? ((L - 68) >> 6) + 1 : 0;
   uint32_t R = L - (k << 6);
   uint32_t e = R > 64 ? 1 : 0;
@@ -97,6 +107,13 @@ __device__ inline uint32_t copy_bytes_cf(uint32_t off, uint32_t L) {
 // the rest as copy-1 (L < 12, off < 2048) or copy-2
 __device__ inline void put_copy_cf(uint8_t* dst, uint32_t o, uint32_t off, uint32_t L) {
   const uint8_t lo = (uint8_t)off, hi = (uint8_t)(off >> 8);
+  if (kShortCopies) {  // L <= 64: one copy-1 or copy-2 (emit_copy_upto_64!, internal.jl:289-304)
+    const bool c1 = L < 12 && off < 2048;
+    dst[o] = (uint8_t)(c1 ? 1 + ((L - 4) << 2) + ((off >> 3) & 0xe0) : 2 + ((L - 1) << 2));
+    dst[o + 1] = lo;
+    if (!c1) dst[o + 2] = hi;
+    return;
+  }
   while (L >= 68) {
     dst[o] = (uint8_t)(2 + (63 << 2));
     dst[o + 1] = lo;
@@ -123,13 +140,6 @@ __device__ inline void put_copy_cf(uint8_t* dst, uint32_t o, uint32_t off, uint3
 
 #ifndef SM_FAST_PRIO
 #define SM_FAST_PRIO 3
-#endif
-// Longest copy the parse takes (0: to the chunk end).  64 is emit_copy!'s own piece size, so a
-// longer match costs the same bytes as 64-byte copies chained through the next positions'
-// candidates; capping bounds the extension loop at four steps (text: 4.13 -> 4.09 ms, ratio
-// 0.5977 -> 0.5978; 128 gains nothing).
-#ifndef SM_FAST_LCAP
-#define SM_FAST_LCAP 64
 #endif
 // Parse waves step their priority down through a round (2 for the previous round's emission,
 // 1 for the first chunk, 0 for the second): the SIMD issues oldest-first among equal
