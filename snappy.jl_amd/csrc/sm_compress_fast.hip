@@ -78,6 +78,10 @@ constexpr uint32_t kBuilt = kChunk == 256 ? SM_FAST_BUILT : kLevels;
 #define SM_FAST_LCAP 64
 #endif
 constexpr bool kShortCopies = SM_FAST_LCAP != 0 && SM_FAST_LCAP <= 64;  // one piece per copy
+#ifndef SM_FAST_XCOMPACT
+#define SM_FAST_XCOMPACT 1
+#endif
+constexpr bool kXCompact = SM_FAST_XCOMPACT && kChunk == 256;  // extension jobs compacted (below)
 
 // literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
 __device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
@@ -278,31 +282,78 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
     offs[j] = q - c;
   }
   // finish matches that filled the 8-byte window: 16 bytes per lane per step
+  auto ext_step = [&](uint32_t q, uint32_t off, uint32_t lim, uint32_t& L, bool& more) {
+    // five aligned dwords per side, four funnel shifts each
+    const uint32_t avail = lim - L;
+    const uint32_t a = q - off + L, b = q + L;
+    const uint32_t* wa = reinterpret_cast<const uint32_t*>(data + (a & ~3u));
+    const uint32_t* wb = reinterpret_cast<const uint32_t*>(data + (b & ~3u));
+    const uint32_t sa = a & 3u, sb = b & 3u;
+    uint32_t x[4];
 #pragma unroll
-  for (int j = 0; j < kP; ++j) {
-    const uint32_t q = c0 + 64 * j + lane;
-    uint32_t L = Ls[j];
-    const uint32_t lim = SM_FAST_LCAP ? min(ce - q, (uint32_t)SM_FAST_LCAP) : ce - q;
-    bool more = !(SM_ABLATE & 8) && L >= 8 && L < lim;
-    while (ballot(more)) {
-      if (more) {
-        // 16 bytes per step: five aligned dwords per side, four funnel shifts each
-        const uint32_t avail = lim - L;
-        const uint32_t a = q - offs[j] + L, b = q + L;
-        const uint32_t* wa = reinterpret_cast<const uint32_t*>(data + (a & ~3u));
-        const uint32_t* wb = reinterpret_cast<const uint32_t*>(data + (b & ~3u));
-        const uint32_t sa = a & 3u, sb = b & 3u;
-        uint32_t x[4];
+    for (int k = 0; k < 4; ++k)
+      x[k] = __builtin_amdgcn_alignbyte(wa[k + 1], wa[k], sa) ^ __builtin_amdgcn_alignbyte(wb[k + 1], wb[k], sb);
+    const uint64_t lo = ((uint64_t)x[1] << 32) | x[0], hi = ((uint64_t)x[3] << 32) | x[2];
+    const uint32_t fb = lo ? (uint32_t)(__builtin_ctzll(lo) >> 3) : (hi ? 8u + (uint32_t)(__builtin_ctzll(hi) >> 3) : 16u);
+    L += min(fb, avail);
+    more = fb == 16 && avail > 16;
+  };
+  auto ext_lim = [&](uint32_t q) { return SM_FAST_LCAP ? min(ce - q, (uint32_t)SM_FAST_LCAP) : ce - q; };
+  if (kXCompact) {
+    // The extensions of all four position groups are compacted into one list first (ballot
+    // prefix into a per-wave LDS scratch: jump-table rows 1-4, free until the doubling), so
+    // the step loop runs over full waves of jobs instead of four partly idle groups; the
+    // lengths come back through row 5.
+    uint32_t* jl = reinterpret_cast<uint32_t*>(jt + kRow);
+    uint8_t* lr = jt + 5 * kRow;
+    uint64_t JM[kP];
+    uint32_t nj = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-          x[k] = __builtin_amdgcn_alignbyte(wa[k + 1], wa[k], sa) ^ __builtin_amdgcn_alignbyte(wb[k + 1], wb[k], sb);
-        const uint64_t lo = ((uint64_t)x[1] << 32) | x[0], hi = ((uint64_t)x[3] << 32) | x[2];
-        const uint32_t fb = lo ? (uint32_t)(__builtin_ctzll(lo) >> 3) : (hi ? 8u + (uint32_t)(__builtin_ctzll(hi) >> 3) : 16u);
-        L += min(fb, avail);
-        more = fb == 16 && avail > 16;
-      }
+    for (int j = 0; j < kP; ++j) {
+      const uint32_t q = c0 + 64 * j + lane;
+      const bool need = !(SM_ABLATE & 8) && Ls[j] >= 8 && Ls[j] < ext_lim(q);  // then Ls[j] == 8
+      JM[j] = ballot(need);
+      if (need)
+        jl[nj + __builtin_amdgcn_mbcnt_hi((uint32_t)(JM[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)JM[j], 0u))] =
+            (64 * j + lane) | (offs[j] << 8);
+      nj += (uint32_t)__builtin_popcountll(JM[j]);
     }
-    Ls[j] = (SM_ABLATE & 2) ? 0u : L;
+    if (nj) {
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      for (uint32_t r0 = 0; r0 < nj; r0 += 64) {
+        const bool act = r0 + lane < nj;
+        const uint32_t d = jl[act ? r0 + lane : 0];
+        const uint32_t pos = d & 0xffu, q = c0 + pos;
+        const uint32_t lim = ext_lim(q);
+        uint32_t L = 8;
+        bool more = act;
+        while (ballot(more)) {
+          if (more) ext_step(q, d >> 8, lim, L, more);
+        }
+        if (act) lr[pos] = (uint8_t)L;
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+      for (int j = 0; j < kP; ++j)
+        if ((JM[j] >> lane) & 1u) Ls[j] = lr[64 * j + lane];
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kP; ++j) {
+      const uint32_t q = c0 + 64 * j + lane;
+      uint32_t L = Ls[j];
+      const uint32_t lim = ext_lim(q);
+      bool more = !(SM_ABLATE & 8) && L >= 8 && L < lim;
+      while (ballot(more)) {
+        if (more) ext_step(q, offs[j], lim, L, more);
+      }
+      Ls[j] = L;
+    }
+  }
+  if (SM_ABLATE & 2) {
+#pragma unroll
+    for (int j = 0; j < kP; ++j) Ls[j] = 0;
   }
   // Greedy parse by pointer doubling (no serial loop) over the chunk's positions.  J0 skips
   // literal runs: J0[r] = the first match position >= r + L(r) (L = 0 for a non-match), else
