@@ -15,13 +15,16 @@
 //    candidates go to a per-round LDS ring, one round ahead of the parse.
 //  * 15 PARSE waves.  The block is cut into kChunk-byte chunks whose parse never crosses the
 //    chunk end (copies are truncated there, literal runs end there), so the chunks of a round
-//    are parsed independently: in round r parse wave w owns chunk 15r+w, kChunk/64 positions
-//    per lane (q = c0 + 64j + lane).  Per chunk: verify and extend the chain candidates of
-//    every position, greedy parse by pointer doubling (J_k = J_{k-1} o J_{k-1}), token sizes
-//    in closed form and a DPP scan, then (after the round barrier) the round layout over the 15
-//    chunks -- literal runs that cross chunk boundaries are merged -- and the emission: token
-//    lanes write tag bytes, position lanes scatter literal bytes.
-// One barrier per round (chunk infos are double-buffered).  Output is deterministic.
+//    are parsed independently: in round r parse wave w owns chunk slots w and w + 15 (fast
+//    mode; slot w in dense mode), kChunk/64 positions per lane (q = c0 + 64j + lane).  Per
+//    chunk: verify the chain candidates of every position (8 bytes) and extend the matches
+//    that fill that window (compacted into full waves of jobs, copies capped at 64 bytes),
+//    greedy parse by pointer doubling (J_k = J_{k-1} o J_{k-1}), token sizes in closed form and
+//    a DPP scan, then (after the round barrier) the round layout over the round's chunks --
+//    literal runs that cross chunk boundaries are merged -- and the emission: token lanes
+//    write tag bytes, position lanes scatter literal bytes.
+// One barrier per round (chunk infos are double-buffered); the parse waves step their issue
+// priority down through a round so they cross it together.  Output is deterministic.
 #include <type_traits>
 
 #include "sm_device.h"
