@@ -262,23 +262,31 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
   // (a) candidates: the latest (and second-latest) earlier position with the same hash,
   // verified and extended 8 bytes at a time; the longest wins (ties: the latest).
   uint32_t Ls[kP], offs[kP];
+  // every group's ring entry and word first, then branch-free verification: every lane reads
+  // its candidate's 8 bytes (an invalid candidate reads its own position), so the LDS round
+  // trips overlap and no exec-mask branches are needed (text: 3.92 -> 3.87 ms)
+  uint32_t cvs[kP];
+  uint64_t wqs[kP];
 #pragma unroll
   for (int j = 0; j < kP; ++j) {
     const uint32_t q = c0 + 64 * j + lane;
-    const uint64_t wq = lds_ld64(data, q < n ? q : 0);  // the 8 bytes at q
+    cvs[j] = cr[64 * j + lane];
+    wqs[j] = lds_ld64(data, q < n ? q : 0);  // the 8 bytes at q
+  }
+#pragma unroll
+  for (int j = 0; j < kP; ++j) {
+    const uint32_t q = c0 + 64 * j + lane;
     const bool can = q + 4 <= ce;
-    const uint32_t cv = cr[64 * j + lane];
     uint32_t L = 0, c = q;
 #pragma unroll
     for (int i = 0; i < kDepth; ++i) {
-      const uint32_t p = (cv >> (16 * i)) & 0xffffu;  // position + 1, 0 = none
-      if (can && p != 0 && p - 1 < q) {
-        const uint64_t x = lds_ld64(data, p - 1) ^ wq;
-        const uint32_t l = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
-        if (l >= 4 && l > L) {
-          L = l;
-          c = p - 1;
-        }
+      const uint32_t p = (cvs[j] >> (16 * i)) & 0xffffu;  // position + 1, 0 = none
+      const bool ok = can && p != 0 && p - 1 < q;
+      const uint64_t x = lds_ld64(data, ok ? p - 1 : q) ^ wqs[j];
+      const uint32_t l = x ? (uint32_t)(__builtin_ctzll(x) >> 3) : 8u;
+      if (ok && l >= 4 && l > L) {
+        L = l;
+        c = p - 1;
       }
     }
     Ls[j] = min(L, ce - q);
