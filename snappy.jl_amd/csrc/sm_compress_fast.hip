@@ -400,12 +400,12 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     uint32_t g[kP];
 #pragma unroll
-    for (int j = 0; j < kP; ++j) g[j] = Ls[j] ? jt[64 * j + lane + Ls[j]] : jv[j];
+    for (int j = 0; j < kP; ++j) g[j] = jt[64 * j + lane + Ls[j]];  // L = 0: NM[r] itself
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 #pragma unroll
     for (int j = 0; j < kP; ++j) {
       jv[j] = g[j];
-      if (Ls[j]) jt[64 * j + lane] = (uint8_t)jv[j];
+      jt[64 * j + lane] = (uint8_t)jv[j];  // unchanged where L = 0
     }
 #pragma unroll
     for (int kk = 1; kk < (int)kBuilt; ++kk) {
