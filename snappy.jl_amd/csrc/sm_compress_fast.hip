@@ -483,10 +483,11 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
   const uint32_t end = tq + tL;
   const uint32_t prev_end = __builtin_amdgcn_update_dpp(0u, end, 0x138, 0xf, 0xf, false);  // wave_shr:1
   t.ls = lane == 0 ? c0 : prev_end;
-  if (lane < t.ntok) {
-    t.litlen = tq - t.ls;
+  {  // selects, not a branch: lanes past the tokens get zeros
+    const bool tok = lane < t.ntok;
+    t.litlen = tok ? tq - t.ls : 0u;
     t.littag = lit_tag_bytes(t.litlen);
-    t.sz = t.littag + t.litlen + (tL ? copy_bytes_cf(t.tb, tL) : 0);
+    t.sz = tok ? t.littag + t.litlen + (tL ? copy_bytes_cf(t.tb, tL) : 0u) : 0u;
   }
   t.incl = scan_dpp(t.sz);
   const uint32_t trail = ce - c0 - last_end;
