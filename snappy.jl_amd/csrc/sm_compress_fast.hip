@@ -532,7 +532,9 @@ __device__ inline void emit_chunk(uint8_t* dst, const uint8_t* data, const Chunk
 #pragma unroll
   for (int j = 0; j < kP; ++j) {
     const uint32_t x = t.c0 + 64 * j + lane;
-    if (x < t.ce && (cnt[j] == 0 || x >= pend[j])) dst[x + dl[j]] = (uint8_t)v[j];  // 32-bit offset: saddr store
+    // one mask (bitwise, so the compiler does not split it into nested branches)
+    const bool lit = (x < t.ce) & ((cnt[j] == 0) | (x >= pend[j]));
+    if (lit) dst[x + dl[j]] = (uint8_t)v[j];  // 32-bit offset: saddr store
   }
 }
 
