@@ -328,17 +328,17 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const uint32_t incl = scan_dpp(osat);
       const uint32_t opt = op + incl - osat;
       const uint32_t lsrc = tpos + 1 + taglen;
-      int32_t err = kOk;
-      if (mine) {
+      // the reference's checks as selects (no exec branches); same first-failing order
+      int32_t err;
+      {
         const int64_t avail_out = (int64_t)size - (int64_t)opt;
-        if (iscopy) {
-          if ((int64_t)opt <= (int64_t)(uint32_t)(offset - 1u)) err = kErrCopyOffset;                    // :499
-          else if (opt - offset < frag_lo) err = kErrCross;
-          else if (!(len <= 16 && offset >= 8 && avail_out >= 16) && avail_out < (int64_t)len) err = kErrCopyLength;  // :505
-        } else {
-          const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
-          if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) err = kErrLiteral;             // :518
-        }
+        const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
+        const bool e_off = (int64_t)opt <= (int64_t)(uint32_t)(offset - 1u);                              // :499
+        const bool e_cross = opt - offset < frag_lo;
+        const bool e_len = !((len <= 16) & (offset >= 8) & (avail_out >= 16)) & (avail_out < (int64_t)len);  // :505
+        const bool e_lit = (avail_out < (int64_t)litlen) | (avail_in < (int64_t)litlen);                   // :518
+        const int32_t ec = e_off ? kErrCopyOffset : (e_cross ? kErrCross : (e_len ? kErrCopyLength : kOk));
+        err = !mine ? kOk : (iscopy ? ec : (e_lit ? kErrLiteral : kOk));
       }
       const uint64_t em = ballot(err != kOk);
       if (em) return (int32_t)readlane((uint32_t)err, ctz64(em));
