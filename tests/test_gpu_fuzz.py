@@ -1,0 +1,85 @@
+"""Randomised round trips of the fast compressor on the GPU: structured blocks of ragged sizes
+(periodic patterns, runs, small alphabets, mutated text, random tails, planted copies at
+random distances) through fast and dense mode, decoded on the GPU and compared byte-for-byte,
+with a sample decoded by the CPU oracle (the reference's decoder restated) as well.  Fast mode
+has no byte-parity target: validity under the reference's decoder is the bar."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import TESTDATA
+
+pytestmark = pytest.mark.gpu
+
+SLOT = 76490 + 8  # sm_max_compressed_length(65536) + slack
+
+
+def gen_block(rng, text):
+    n = int(rng.choice([rng.integers(1, 300), rng.integers(300, 65537), 65536]))
+    kind = int(rng.integers(0, 6))
+    if kind == 0:  # periodic pattern, random period
+        b = np.resize(rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8), n)
+    elif kind == 1:  # runs of random bytes and lengths
+        out, tot = [], 0
+        while tot < n:
+            L = int(rng.integers(1, 200))
+            out.append(np.full(L, rng.integers(0, 256), np.uint8))
+            tot += L
+        b = np.concatenate(out)[:n]
+    elif kind == 2:  # small alphabet
+        b = rng.integers(0, int(rng.integers(2, 5)), n, dtype=np.uint8)
+    elif kind == 3:  # mutated text
+        s = int(rng.integers(0, text.size - n)) if text.size > n else 0
+        b = text[s:s + n].copy()
+        m = rng.random(b.size) < rng.choice([0.0, 0.001, 0.05])
+        b[m] = rng.integers(0, 256, int(m.sum()), dtype=np.uint8)
+    elif kind == 4:  # text, then a random tail
+        s = int(rng.integers(0, max(1, text.size - n)))
+        b = text[s:s + n].copy()
+        cut = int(rng.integers(0, b.size + 1))
+        b[cut:] = rng.integers(0, 256, b.size - cut, dtype=np.uint8)
+    else:  # random bytes with planted copies (long and overlapping matches)
+        b = rng.integers(0, 256, n, dtype=np.uint8)
+        for _ in range(int(rng.integers(1, 40))):
+            L, d = int(rng.integers(4, 300)), int(rng.integers(1, 2000))
+            p = int(rng.integers(0, max(1, n - L)))
+            for k in range(min(L, n - p)):
+                if p + k - d >= 0:
+                    b[p + k] = b[p + k - d]
+    return np.ascontiguousarray(b[:n], dtype=np.uint8)
+
+
+# more seeds for a longer run: SM_FUZZ_SEEDS=40
+@pytest.mark.parametrize("seed", range(1, 1 + int(os.environ.get("SM_FUZZ_SEEDS", "3"))))
+def test_fast_modes_random_structured_blocks(sm, oracle, gpu_available, seed):
+    import torch
+    rng = np.random.default_rng(seed)
+    text = np.frombuffer(open(os.path.join(TESTDATA, "lcet10.txt"), "rb").read(), np.uint8)
+    blocks = [gen_block(rng, text) for _ in range(1500)]
+    lens = np.array([b.size for b in blocks], np.int64)
+    off = np.zeros(len(blocks), np.int64)
+    off[1:] = np.cumsum(lens[:-1])
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(np.concatenate(blocks)).to(dev)
+    in_off = torch.from_numpy(off).to(dev)
+    in_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    comp_off = torch.arange(len(blocks), dtype=torch.int64, device=dev) * SLOT
+    for mode in ("fast", "dense"):
+        d_comp = torch.zeros(len(blocks) * SLOT, dtype=torch.uint8, device=dev)
+        comp_len = torch.zeros(len(blocks), dtype=torch.int32, device=dev)
+        sm.compress_batch_device(d_in, in_off, in_len, d_comp, comp_off, comp_len, mode=mode)
+        d_dec = torch.zeros_like(d_in)
+        dec_len = torch.zeros_like(in_len)
+        status = torch.zeros_like(in_len)
+        sm.uncompress_batch_device(d_comp, comp_off, comp_len, d_dec, in_off, in_len, dec_len, status)
+        torch.cuda.synchronize()
+        assert int(status.abs().sum()) == 0
+        assert torch.equal(dec_len, in_len)
+        assert torch.equal(d_dec, d_in)
+        cl = comp_len.cpu().numpy()
+        assert (cl.astype(np.int64) <= 32 + lens + lens // 6 + 5).all()  # within maxlength + header
+        host = d_comp.cpu().numpy()
+        for k in rng.choice(len(blocks), 60, replace=False):
+            s = host[k * SLOT: k * SLOT + int(cl[k])].tobytes()
+            assert oracle.uncompress(s) == blocks[k].tobytes(), (mode, int(k))
