@@ -218,17 +218,23 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, typename C
     const uint32_t base = r0 + 64 * g0;
     uint32_t old[kG], hn[kG];
     bool okn[kG];
+    if (full) {  // a uniform branch: every lane exchanges, no per-exchange exec masks
 #pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      old[i] = 0;
-      if (full || ok[i])
+      for (int i = 0; i < kG; ++i)
         old[i] = __hip_atomic_exchange(&T[h[i]], base + 64 * i + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+#pragma unroll
+      for (int i = 0; i < kG; ++i) {
+        old[i] = 0;
+        if (ok[i])
+          old[i] = __hip_atomic_exchange(&T[h[i]], base + 64 * i + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
     }
     if (g0 + kG < ngroups) hash_step(g0 + kG, hn, okn);
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
       // the old latest becomes the second-latest (the new entry's high half)
-      if (D > 1 && (full || ok[i])) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];
+      if (D > 1 && (full || ok[i])) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];  // (dense only)
       ring[64 * (g0 + i) + lane] = (typename Cfg<D>::Cand)old[i];
     }
 #pragma unroll
