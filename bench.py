@@ -1,31 +1,46 @@
 """Benchmark: batched 64 KiB-block snappy compress + uncompress on MI355X (BASELINE.json).
 
-Workload (BASELINE.json configs[1] + configs[2]): 10,000 blocks of
-65,536 B, block i = the 64 KiB window at offset o_i ~ U[0, L-65536) of alice29 + asyoulik +
-lcet10 + plrabn12 (L = 1,185,883), o_i from numpy default_rng(0x5EED + rank).  Inputs are
-resident in HBM before timing starts.
+`python bench.py --gpus N --steps K --warmup W`.  With N > 1 and no WORLD_SIZE in the
+environment the script starts N ranks itself (torch.distributed.run, before any GPU call) and
+exits with their status; under torchrun it checks WORLD_SIZE == N and that the node has N GPUs,
+and exits non-zero otherwise.  One process per GPU, RCCL for the collectives.
 
-One step = fast-mode batched compress of the 10K blocks (each an independent snappy stream
-in a fixed 76,496-B slot) -> [N>1: RCCL all-gather of the u32 compressed sizes] -> batched
-uncompress of those slots back into 64 KiB blocks.  value = (uncompressed bytes compressed +
-uncompressed bytes decompressed) per second, summed over ranks (weak scaling: every rank
-owns its own 10K blocks).  After timing, the round trip is checked bit-exactly on the device.
+Workloads (BASELINE.json configs):
+* headline (`value`), configs 2+3: every rank owns 10,000 blocks of 65,536 B, block i = the
+  64 KiB window at offset o_i ~ U[0, L-65536) of alice29 + asyoulik + lcet10 + plrabn12
+  (L = 1,185,883), o_i from numpy default_rng(0x5EED + rank).  One step = fast-mode batched
+  compress (each block an independent snappy stream in a fixed 76,496-B slot) -> [N > 1: RCCL
+  all-gather of the u32 compressed sizes] -> batched uncompress back into 64 KiB blocks.
+  value = (uncompressed bytes compressed + uncompressed bytes decompressed) / s summed over
+  ranks: weak scaling.
+* `random` (config 4): 10,000 uniform random blocks per rank (default_rng(0x5EED + 1 + rank)),
+  the same step.
+* `large` (config 5): ONE 644 MiB stream (the 15 round-trip corpus files tiled with seeded
+  rotations, exactly 10,304 fragments), strong-scaled: rank r owns the contiguous fragments
+  shard_range(10304, r, N).  One step = fast-mode compress of the rank's fragments (no headers,
+  Q2 table size) -> RCCL all-gather of the u32 fragment sizes + exclusive scan = every
+  fragment's global offset behind the varint header -> uncompress of the rank's fragments.
+Inputs are resident in HBM before timing starts.  Every workload is timed over K steps between
+a barrier + device synchronize on both sides, max over ranks, and its round trip is checked
+bit-exactly on the device afterwards.
 
-roofline: the dominant kernel's algorithmic HBM bytes per launch (compress: sum N read +
-sum C written; uncompress: sum C read + sum N written) / its average duration from HIP events
-on the launch stream, against 8.0 TB/s.  traffic: from profiles/<round>_pmc.json if present.
-cpu_baseline: the oracle (C restatement of Snappy.jl, reference mode) on a bounded sample,
-OpenMP over blocks on the host cores, rank 0 only.
+roofline: a kernel's algorithmic HBM bytes per launch (compress: sum N read + sum C written +
+4 B of size per block; uncompress: sum C read + sum N written) / its median launch duration from
+HIP events on the launch stream, against 8.0 TB/s.  traffic: profiles/<round>_pmc.json (rocprofv3
+FETCH_SIZE/WRITE_SIZE passes) when present.  cpu_baseline (rank 0): the oracle (C restatement of
+Snappy.jl, reference mode) and libsnappy 1.1.8, OpenMP over blocks on every core this process
+may use, on a bounded sample of the headline workload.
 """
 import argparse
 import importlib.util
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 import numpy as np
-import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 TESTDATA = os.path.join(ROOT, "tests", "golden", "testdata")
@@ -34,7 +49,13 @@ BLOCK = 65536
 SLOT = 76496  # >= max_compressed_length(65536) = 76490, 16-B aligned
 HBM_PEAK_GBPS = 8000.0
 METRIC = "GB/s compressed+decompressed (batched blocks) at 1/2/4/8 GPUs; % HBM peak"  # BASELINE.json
-ROUND = "r01"
+ROUND = "r02"
+
+# test/runtests.jl:8-24, the round-trip corpus; config 5 tiles it (SURVEY §8(d))
+ROUNDTRIP_FILES = ["alice29.txt", "asyoulik.txt", "html", "html_x_4", "kppkn.gtb", "lcet10.txt", "fireworks.jpeg",
+                   "geo.protodata", "paper-100k.pdf", "plrabn12.txt", "urls.10K", "random1.bin", "random2.bin",
+                   "random3.bin", "smallrandom1.bin"]
+CONFIG5_BYTES = 675_282_944  # 644 MiB = exactly 10,304 blocks
 
 
 def load_package():
@@ -47,11 +68,11 @@ def load_package():
     return mod
 
 
-# test/runtests.jl:8-24, the round-trip corpus; config 5 tiles it (SURVEY §8(d))
-ROUNDTRIP_FILES = ["alice29.txt", "asyoulik.txt", "html", "html_x_4", "kppkn.gtb", "lcet10.txt", "fireworks.jpeg",
-                   "geo.protodata", "paper-100k.pdf", "plrabn12.txt", "urls.10K", "random1.bin", "random2.bin",
-                   "random3.bin", "smallrandom1.bin"]
-CONFIG5_BYTES = 675_282_944  # 644 MiB = exactly 10,304 blocks
+def load_dist():
+    spec = importlib.util.spec_from_file_location("snappy_jl_amd_dist", os.path.join(ROOT, "snappy.jl_amd", "dist.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
 
 
 def large_corpus(nbytes=CONFIG5_BYTES, seed=0x5EED + 5):
@@ -86,14 +107,36 @@ def random_blocks(nblk, seed):
     return rng.integers(0, 256, (nblk, BLOCK), dtype=np.uint8)
 
 
+# ---- launching ranks ----------------------------------------------------------------------
+
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run (this process
+    has not touched the GPU; torch.cuda.device_count() does not initialise it on this image)."""
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev < args.gpus:
+        print("bench.py: --gpus %d but only %d GPU(s) visible" % (args.gpus, ndev), file=sys.stderr)
+        return 2
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+# ---- device workloads -----------------------------------------------------------------------
+
 class Batch:
-    """Device-resident batch: inputs, fixed compressed slots, decode targets."""
+    """Device-resident batch of independent blocks: inputs, fixed compressed slots, decode targets."""
 
     def __init__(self, blocks_np, dev):
+        import torch
         nblk = blocks_np.shape[0]
         self.nblk = nblk
+        self.in_bytes = nblk * BLOCK
         self.d_in = torch.from_numpy(blocks_np.reshape(-1)).to(dev)
-        self.in_off = (torch.arange(nblk, dtype=torch.int64, device=dev) * BLOCK)
+        self.in_off = torch.arange(nblk, dtype=torch.int64, device=dev) * BLOCK
         self.in_len = torch.full((nblk,), BLOCK, dtype=torch.int32, device=dev)
         self.d_comp = torch.empty(nblk * SLOT, dtype=torch.uint8, device=dev)
         self.comp_off = torch.arange(nblk, dtype=torch.int64, device=dev) * SLOT
@@ -103,7 +146,7 @@ class Batch:
         self.dec_len = torch.zeros(nblk, dtype=torch.int32, device=dev)
         self.status = torch.zeros(nblk, dtype=torch.int32, device=dev)
 
-    def compress(self, sm, mode):
+    def compress(self, sm, mode="fast"):
         sm.compress_batch_device(self.d_in, self.in_off, self.in_len, self.d_comp, self.comp_off, self.comp_len,
                                  mode=mode)
 
@@ -111,17 +154,232 @@ class Batch:
         sm.uncompress_batch_device(self.d_comp, self.comp_off, self.comp_len, self.d_dec, self.in_off, self.dec_cap,
                                    self.dec_len, self.status)
 
+    def comp_bytes(self):
+        import torch
+        return int(self.comp_len.to(torch.int64).sum())
+
     def verify(self):
+        import torch
+        self.d_dec.fill_(0xAA)
+        self.uncompress(load_package_cached())
         ok = bool(torch.equal(self.d_dec, self.d_in)) and int(self.status.abs().sum()) == 0
-        ok = ok and bool((self.dec_len == BLOCK).all())
+        return ok and bool((self.dec_len == self.in_len).all())
+
+
+class StreamShard:
+    """Config 5: this rank's fragments of ONE stream (no per-fragment header, table size of the
+    whole stream), their compressed slots, the global index, and decode targets."""
+
+    def __init__(self, stream_np, lo, hi, dev):
+        import torch
+        total = stream_np.size
+        self.total = total
+        self.lo, self.hi = lo, hi
+        nf = hi - lo
+        self.nfrag = nf
+        a, b = lo * BLOCK, min(hi * BLOCK, total)
+        self.in_bytes = b - a
+        lens = np.minimum(BLOCK, total - np.arange(lo, hi, dtype=np.int64) * BLOCK)
+        self.d_in = torch.from_numpy(np.ascontiguousarray(stream_np[a:b])).to(dev)
+        self.in_off = torch.arange(nf, dtype=torch.int64, device=dev) * BLOCK
+        self.in_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        self.d_comp = torch.empty(max(nf, 1) * SLOT, dtype=torch.uint8, device=dev)
+        self.comp_off = torch.arange(nf, dtype=torch.int64, device=dev) * SLOT
+        self.comp_len = torch.zeros(nf, dtype=torch.int32, device=dev)
+        self.d_dec = torch.empty(max(self.in_bytes, 1), dtype=torch.uint8, device=dev)
+        self.dec_len = torch.zeros(nf, dtype=torch.int32, device=dev)
+        self.status = torch.zeros(nf, dtype=torch.int32, device=dev)
+        self.offsets = None
+        self.stream_len = None
+
+    def compress(self, sm):
+        sm.compress_fragments_device(self.d_in, self.in_off, self.in_len, self.d_comp, self.comp_off, self.comp_len,
+                                     self.total, mode="fast")
+
+    def index(self, dist_mod, rank, world):
+        self.offsets, self.stream_len = dist_mod.stream_offsets_device(self.comp_len, self.total, rank, world)
+
+    def uncompress(self, sm):
+        sm.uncompress_fragments_device(self.d_comp, self.comp_off, self.comp_len, self.d_dec, self.in_off,
+                                       self.in_len, self.dec_len, self.status)
+
+    def verify(self, sm):
+        import torch
+        self.d_dec.fill_(0xAA)
+        self.uncompress(sm)
+        ok = bool(torch.equal(self.d_dec[: self.in_bytes], self.d_in)) and int(self.status.abs().sum()) == 0
+        ok = ok and bool((self.dec_len == self.in_len).all())
+        # the global index: offsets strictly increasing by this rank's sizes
+        if self.nfrag > 1:
+            d = self.offsets[1:] - self.offsets[:-1]
+            ok = ok and bool(torch.equal(d, self.comp_len[:-1].to(torch.int64)))
         return ok
 
 
-def config5_stream(sm, reps=3):
+_SM = None
+
+
+def load_package_cached():
+    global _SM
+    if _SM is None:
+        _SM = load_package()
+    return _SM
+
+
+def timed_steps(step, steps, warmup, world, dist, dev):
+    """W untimed steps, then K steps between barrier + synchronize on both sides; max over ranks."""
+    import torch
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def kernel_ms(fn, reps):
+    """Median launch duration (ms) of fn from HIP events on the launch stream (torch's current
+    stream, which every sm.*_device call launches on)."""
+    import torch
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    fn()
+    torch.cuda.synchronize()
+    for s, e in ev:
+        s.record()
+        fn()
+        e.record()
+    torch.cuda.synchronize()
+    return float(np.median([s.elapsed_time(e) for s, e in ev]))
+
+
+def pmc_traffic(kernel):
+    path = os.path.join(ROOT, "profiles", ROUND + "_pmc.json")
+    try:
+        return json.load(open(path)).get(kernel, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def roofline(kernel, alg_bytes, ms):
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    return {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": pmc_traffic(kernel),
+            "algorithmic_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4)}
+
+
+# ---- CPU baseline ----------------------------------------------------------------------------
+
+def cpu_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(blocks_np, nblk=2048, reps=10, single_reps=3):
+    """The oracle (Snappy.jl's algorithm restated in C, reference mode) and libsnappy 1.1.8, both
+    OpenMP over blocks on every core this process may use, on the first nblk blocks of the
+    headline workload; median over reps passes (single-thread figures: median over single_reps)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    threads = cpu_cores()
+    sample = np.ascontiguousarray(blocks_np[:nblk])
+    nblk = sample.shape[0]
+    inp = sample.reshape(-1)
+    in_off = np.arange(nblk, dtype=np.uint64) * BLOCK
+    in_len = np.full(nblk, BLOCK, dtype=np.uint32)
+    comp = np.empty(nblk * SLOT, dtype=np.uint8)
+    comp_off = np.arange(nblk, dtype=np.uint64) * SLOT
+    comp_cap = np.full(nblk, SLOT, dtype=np.uint32)
+    comp_len = np.zeros(nblk, dtype=np.uint32)
+    dec = np.empty(nblk * BLOCK, dtype=np.uint8)
+    dec_len = np.zeros(nblk, dtype=np.uint32)
+    st = np.zeros(nblk, dtype=np.int32)
+    nbytes = inp.size
+
+    def med(fn, n):
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return float(np.median(ts))
+
+    def oracle_rates(th, n):
+        tc = med(lambda: O.compress_batch(inp, in_off, in_len, comp, comp_off, comp_len, compat=False, nthreads=th), n)
+        td = med(lambda: O.uncompress_batch(comp, comp_off, comp_len, dec, in_off, in_len, dec_len, st, nthreads=th), n)
+        assert np.array_equal(dec, inp) and not st.any()
+        return nbytes / tc / 1e9, nbytes / td / 1e9
+
+    c_all, d_all = oracle_rates(threads, reps)
+    c_one, d_one = oracle_rates(1, single_reps)
+    res = {
+        "value": round(2 / (1 / c_all + 1 / d_all), 4),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": "%d x 64 KiB text blocks (the first %d of the headline workload); reference-mode compress + "
+                  "uncompress by oracle/snappy_oracle.c (-O3, OpenMP over blocks on %d threads = every core this "
+                  "process may use; os.cpu_count() = %d, %s); median of %d passes" % (
+                      nblk, nblk, threads, os.cpu_count() or 0, cpu_model(), reps),
+        "compress_GBps": round(c_all, 4),
+        "uncompress_GBps": round(d_all, 4),
+        "single_thread_compress_GBps": round(c_one, 4),
+        "single_thread_uncompress_GBps": round(d_one, 4),
+        "host_cpu": cpu_model(),
+        "host_cpu_count": os.cpu_count(),
+    }
+    if O.libsnappy_batch() is not None:
+        def lib_rates(th, n):
+            tc = med(lambda: O.libsnappy_compress_batch(inp, in_off, in_len, comp, comp_off, comp_cap, comp_len, th), n)
+            td = med(lambda: O.libsnappy_uncompress_batch(comp, comp_off, comp_len, dec, in_off, in_len, dec_len, th),
+                     n)
+            assert np.array_equal(dec, inp)
+            return nbytes / tc / 1e9, nbytes / td / 1e9
+        lc, ld = lib_rates(threads, reps)
+        lc1, ld1 = lib_rates(1, single_reps)
+        res["libsnappy_1.1.8"] = {
+            "compress_GBps": round(lc, 4), "uncompress_GBps": round(ld, 4),
+            "roundtrip_GBps": round(2 / (1 / lc + 1 / ld), 4), "threads": threads,
+            "single_thread_compress_GBps": round(lc1, 4), "single_thread_uncompress_GBps": round(ld1, 4),
+        }
+        # README.md:37-45: Julia Snappy.jl is 3.8-48.7% slower than the libsnappy ccall, per file
+        res["julia_estimate_single_thread"] = {
+            "note": "ESTIMATE, not measured: libsnappy single-thread / (1.038 .. 1.487), the Julia/ccall "
+                    "ratio range of the reference README.md:37-45",
+            "compress_GBps": [round(lc1 / 1.487, 4), round(lc1 / 1.038, 4)],
+            "uncompress_GBps": [round(ld1 / 1.487, 4), round(ld1 / 1.038, 4)],
+        }
+    return res
+
+
+def config5_host_stream(sm, big, reps=3):
     """Config 5 as ONE stream through the single-buffer C entry points (sm_compress /
-    sm_uncompress), host buffers allocated and touched once: PCIe-inclusive GB/s, best of reps."""
+    sm_uncompress) from host buffers: PCIe-inclusive GB/s, best of reps."""
     import ctypes
-    big = large_corpus()
     n = big.size
     L, ctx = sm.lib(), sm.context(0)
     cap = sm.maxlength_compressed(n)
@@ -139,90 +397,38 @@ def config5_stream(sm, reps=3):
         st2 = L.sm_uncompress(ctx, comp.ctypes.data, cl.value, back.ctypes.data, ctypes.byref(bl))
         td.append(time.perf_counter() - t0)
     good = st == 0 and st2 == 0 and bl.value == n and bool(np.array_equal(back, big))
-    return {"config5_stream_host_compress_GBps": round(n / min(tc[1:]) / 1e9, 3),
-            "config5_stream_host_uncompress_GBps": round(n / min(td[1:]) / 1e9, 3),
-            "config5_stream_ratio": round(cl.value / n, 5),
-            "config5_stream_ok": good and sm.last_uncompress_path() == 1}
-
-
-def time_kernel(fn, reps):
-    """Average duration (ms) of fn's launches from HIP events on torch's current stream."""
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    s.record()
-    for _ in range(reps):
-        fn()
-    e.record()
-    e.synchronize()
-    return s.elapsed_time(e) / reps
-
-
-def cpu_baseline(blocks_np, seconds=10.0):
-    """Oracle (Snappy.jl restated in C, reference mode) round trip on a bounded sample."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    nthreads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    sample = np.ascontiguousarray(blocks_np[:512])
-    nblk = sample.shape[0]
-    inp = sample.reshape(-1)
-    in_off = (np.arange(nblk, dtype=np.uint64) * BLOCK)
-    in_len = np.full(nblk, BLOCK, dtype=np.uint32)
-    comp = np.empty(nblk * SLOT, dtype=np.uint8)
-    comp_off = np.arange(nblk, dtype=np.uint64) * SLOT
-    comp_len = np.zeros(nblk, dtype=np.uint32)
-    dec = np.empty(nblk * BLOCK, dtype=np.uint8)
-    cap = np.full(nblk, BLOCK, dtype=np.uint32)
-    dec_len = np.zeros(nblk, dtype=np.uint32)
-    st = np.zeros(nblk, dtype=np.int32)
-
-    def run(threads, budget):
-        tc = td = 0.0
-        reps = 0
-        t_end = time.perf_counter() + budget
-        while True:
-            t0 = time.perf_counter()
-            O.compress_batch(inp, in_off, in_len, comp, comp_off, comp_len, compat=False, nthreads=threads)
-            t1 = time.perf_counter()
-            O.uncompress_batch(comp, comp_off, comp_len, dec, in_off, cap, dec_len, st, nthreads=threads)
-            t2 = time.perf_counter()
-            tc += t1 - t0
-            td += t2 - t1
-            reps += 1
-            if time.perf_counter() > t_end:
-                break
-        assert np.array_equal(dec, inp)
-        nbytes = reps * inp.size
-        return tc, td, nbytes, reps
-
-    tc, td, nbytes, reps = run(nthreads, seconds)
-    tc1, td1, nb1, _ = run(1, 3.0)
-    return {
-        "value": round(2 * nbytes / (tc + td) / 1e9, 4),
-        "unit": "GB/s",
-        "cores": nthreads,
-        "kind": "port",
-        "sample": "%d x 64 KiB text blocks (first %d of the workload), %d passes of reference-mode "
-                  "compress + uncompress, oracle/snappy_oracle.c -O3, OpenMP over blocks" % (nblk, nblk, reps),
-        "compress_GBps": round(nbytes / tc / 1e9, 4),
-        "uncompress_GBps": round(nbytes / td / 1e9, 4),
-        "single_thread_compress_GBps": round(nb1 / tc1 / 1e9, 4),
-        "single_thread_uncompress_GBps": round(nb1 / td1 / 1e9, 4),
-    }
+    return {"host_compress_GBps": round(n / min(tc[1:]) / 1e9, 3),
+            "host_uncompress_GBps": round(n / min(td[1:]) / 1e9, 3),
+            "ratio": round(cl.value / n, 5),
+            "ok": good and sm.last_uncompress_path() == 1}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--blocks", type=int, default=10000)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--extras", action="store_true", help="also time reference mode and random blocks")
+    ap.add_argument("--no-large", action="store_true", help="skip the config-5 (644 MiB stream) workload")
+    ap.add_argument("--no-random", action="store_true", help="skip the config-4 (random blocks) workload")
+    ap.add_argument("--extras", action="store_true", help="also time dense/reference modes, validation and the "
+                                                          "PCIe-inclusive single-stream entry points")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    import torch
+    ndev = torch.cuda.device_count()
+    if ndev <= local_rank:
+        print("bench.py: rank %d needs GPU %d but %d visible" % (rank, local_rank, ndev), file=sys.stderr)
+        sys.exit(2)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -230,106 +436,127 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
-    sm = load_package()
+    sm = load_package_cached()
     sm.context(local_rank)
+    dmod = load_dist()
+    reps = max(10, min(args.steps, 20))
+    ok_all = True
 
+    # ---- headline: configs 2 + 3, weak scaling -------------------------------------------
     blocks_np = text_blocks(args.blocks, 0x5EED + rank)
     batch = Batch(blocks_np, dev)
-    sizes_all = None
-    if world > 1:
-        sizes_all = torch.zeros(world * args.blocks, dtype=torch.int32, device=dev)
+    sizes_all = torch.zeros(world * args.blocks, dtype=torch.int32, device=dev) if world > 1 else None
 
     def step():
-        batch.compress(sm, "fast")
+        batch.compress(sm)
         if world > 1:
             dist.all_gather_into_tensor(sizes_all, batch.comp_len)
         batch.uncompress(sm)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed = timed_steps(step, args.steps, args.warmup, world, dist, dev)
+    comp_bytes = batch.comp_bytes()
+    in_bytes = batch.in_bytes
+    t_c = kernel_ms(lambda: batch.compress(sm), reps)
+    t_d = kernel_ms(lambda: batch.uncompress(sm), reps)
     ok = batch.verify()
-    comp_bytes = int(batch.comp_len.to(torch.int64).sum())
-    in_bytes = args.blocks * BLOCK
-
-    # per-kernel durations (HIP events on the launch stream = torch current stream)
-    reps = max(3, min(args.steps, 10))
-    t_c = time_kernel(lambda: batch.compress(sm, "fast"), reps)
-    t_d = time_kernel(lambda: batch.uncompress(sm), reps)
+    ok_all &= ok
     c_bytes = in_bytes + comp_bytes + 4 * args.blocks
     d_bytes = comp_bytes + in_bytes
     kern = {"compress_fast": (t_c, c_bytes), "uncompress": (t_d, d_bytes)}
     dom = max(kern, key=lambda k: kern[k][0])
-    dom_ms, dom_bytes = kern[dom]
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    pmc_path = os.path.join(ROOT, "profiles", ROUND + "_pmc.json")
-    if os.path.exists(pmc_path):
-        try:
-            traffic = json.load(open(pmc_path)).get(dom, {}).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    value = 2.0 * in_bytes * args.steps * world / elapsed / 1e9
 
     extras = {}
     if args.extras:
-        # validation (the decoder's walk + checks, no output) of the fast streams
-        # SM_MODE_FAST_DENSE: two chain candidates per position (smaller output, slower)
-        t_dc = time_kernel(lambda: batch.compress(sm, "dense"), 3)
-        extras["dense_compress_GBps"] = round(in_bytes / (t_dc * 1e-3) / 1e9, 3)
-        extras["dense_ratio"] = round(int(batch.comp_len.to(torch.int64).sum()) / in_bytes, 5)
-        t_dd = time_kernel(lambda: batch.uncompress(sm), 3)
-        ok = ok and batch.verify()
-        extras["dense_streams_uncompress_GBps"] = round(in_bytes / (t_dd * 1e-3) / 1e9, 3)
-        batch.compress(sm, "fast")
-        vst = torch.full_like(batch.status, -1)
-        t_v = time_kernel(lambda: sm.validate_batch_device(batch.d_comp, batch.comp_off, batch.comp_len, vst), 3)
-        ok = ok and int(vst.abs().sum()) == 0
-        extras["validate_GBps"] = round(in_bytes / (t_v * 1e-3) / 1e9, 3)
-        t_ref = time_kernel(lambda: batch.compress(sm, "reference"), 1)
-        extras["reference_mode_compress_GBps"] = round(in_bytes / (t_ref * 1e-3) / 1e9, 3)
-        # config 3 with the exact (Snappy.jl byte-identical) streams as input
-        t_rd3 = time_kernel(lambda: batch.uncompress(sm), 3)
-        ok = ok and batch.verify()
-        extras["reference_streams_uncompress_GBps"] = round(in_bytes / (t_rd3 * 1e-3) / 1e9, 3)
-        extras["reference_ratio"] = round(int(batch.comp_len.to(torch.int64).sum()) / in_bytes, 5)
-        del batch
-        torch.cuda.empty_cache()
-        rb = Batch(random_blocks(args.blocks, 0x5EED + 1 + rank), dev)
-        t_rc = time_kernel(lambda: rb.compress(sm, "fast"), 3)
-        t_rd = time_kernel(lambda: rb.uncompress(sm), 3)
-        rb_comp = int(rb.comp_len.to(torch.int64).sum())
-        ok = ok and rb.verify()
-        extras["random_compress_fast_GBps"] = round(in_bytes / (t_rc * 1e-3) / 1e9, 3)
-        extras["random_uncompress_GBps"] = round(in_bytes / (t_rd * 1e-3) / 1e9, 3)
-        extras["random_ratio"] = round(rb_comp / in_bytes, 5)
-        t_rr = time_kernel(lambda: rb.compress(sm, "reference"), 1)
-        extras["random_reference_compress_GBps"] = round(in_bytes / (t_rr * 1e-3) / 1e9, 3)
+        extras.update(extra_modes(sm, batch, in_bytes))
+    del batch
+    torch.cuda.empty_cache()
 
-    if args.extras and rank == 0:
-        extras.update(config5_stream(sm))
-        ok = ok and extras["config5_stream_ok"]
+    # ---- config 4: incompressible blocks ------------------------------------------------
+    rnd = None
+    if not args.no_random:
+        rb = Batch(random_blocks(args.blocks, 0x5EED + 1 + rank), dev)
+
+        def rstep():
+            rb.compress(sm)
+            rb.uncompress(sm)
+        r_el = timed_steps(rstep, args.steps, args.warmup, world, dist, dev)
+        rc_bytes = rb.comp_bytes()
+        rt_c = kernel_ms(lambda: rb.compress(sm), reps)
+        rt_d = kernel_ms(lambda: rb.uncompress(sm), reps)
+        r_ok = rb.verify()
+        ok_all &= r_ok
+        rnd = {
+            "workload": "config 4: %d x 64 KiB uniform random blocks per GPU (default_rng(0x5EED+1+rank)), "
+                        "fast-mode compress + uncompress per step" % args.blocks,
+            "GBps": round(2.0 * rb.in_bytes * args.steps * world / r_el / 1e9, 3),
+            "ms_per_step": round(r_el / args.steps * 1e3, 4),
+            "compress_GBps": round(rb.in_bytes / (rt_c * 1e-3) / 1e9, 3),
+            "uncompress_GBps": round(rb.in_bytes / (rt_d * 1e-3) / 1e9, 3),
+            "ratio": round(rc_bytes / rb.in_bytes, 6),
+            "roundtrip_bit_exact": r_ok,
+            "roofline": roofline("compress_fast_random", rb.in_bytes + rc_bytes + 4 * args.blocks, rt_c),
+            "roofline_uncompress": roofline("uncompress_random", rb.in_bytes + rc_bytes, rt_d),
+        }
+        del rb
+        torch.cuda.empty_cache()
+
+    # ---- config 5: one 644 MiB stream, strong scaling --------------------------------------
+    large = None
+    big = None
+    if not args.no_large:
+        big = large_corpus()
+        nfrag = (big.size + BLOCK - 1) // BLOCK
+        lo, hi = dmod.shard_range(nfrag, rank, world)
+        sh = StreamShard(big, lo, hi, dev)
+
+        def lstep():
+            sh.compress(sm)
+            sh.index(dmod, rank, world)
+            sh.uncompress(sm)
+        l_el = timed_steps(lstep, args.steps, args.warmup, world, dist, dev)
+        sh.index(dmod, rank, world)
+        lt_c = kernel_ms(lambda: sh.compress(sm), reps)
+        lt_d = kernel_ms(lambda: sh.uncompress(sm), reps)
+        l_ok = sh.verify(sm)
+        ok_all &= l_ok
+        lc_local = int(sh.comp_len.to(torch.int64).sum())
+        stream_len = int(sh.stream_len.item())
+        per_rank_ms = l_el / args.steps * 1e3
+        large = {
+            "workload": "config 5: one %d-B (644 MiB) stream = %d fragments, %d..%d per GPU (contiguous shards); "
+                        "per step: fast-mode fragment compress + RCCL all-gather of the u32 fragment sizes + "
+                        "offset scan + fragment uncompress" % (big.size, nfrag, nfrag // world,
+                                                                (nfrag + world - 1) // world),
+            "scaling": "strong",
+            "GBps": round(2.0 * big.size * args.steps / l_el / 1e9, 3),
+            "ms_per_step": round(per_rank_ms, 4),
+            "fragments_rank0": hi - lo,
+            "compress_GBps_per_gpu": round(sh.in_bytes / (lt_c * 1e-3) / 1e9, 3),
+            "uncompress_GBps_per_gpu": round(sh.in_bytes / (lt_d * 1e-3) / 1e9, 3),
+            "stream_bytes": stream_len,
+            "ratio": round(stream_len / big.size, 5),
+            "roundtrip_bit_exact": l_ok,
+            "roofline": roofline("compress_fragments", sh.in_bytes + lc_local + 4 * sh.nfrag, lt_c),
+        }
+        del sh
+        torch.cuda.empty_cache()
+
+    if args.extras and rank == 0 and world == 1:
+        if big is None:
+            big = large_corpus()
+        extras["config5_host_stream"] = config5_host_stream(sm, big)
+        ok_all &= extras["config5_host_stream"]["ok"]
+
+    if world > 1:
+        t = torch.tensor([0 if ok_all else 1], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ok_all = int(t.item()) == 0
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:
         cpu = cpu_baseline(blocks_np)
 
-    value = 2.0 * in_bytes * args.steps * world / elapsed / 1e9
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -345,7 +572,8 @@ def main():
             "dtype": "u8",
             "data": "synthetic: 64 KiB windows of the Calgary text files in tests/golden/testdata",
             "config": {
-                "workload": "10K x 64 KiB text blocks: fast-mode compress + uncompress round trip per step",
+                "workload": "configs 2+3: %d x 64 KiB text blocks per GPU, fast-mode compress + uncompress round "
+                            "trip per step" % args.blocks,
                 "blocks_per_gpu": args.blocks,
                 "block_bytes": BLOCK,
                 "parallelism": "dp%d (blocks sharded per rank, RCCL size all-gather)" % world,
@@ -354,25 +582,44 @@ def main():
             "uncompress_GBps": round(in_bytes / (t_d * 1e-3) / 1e9, 3),
             "ratio": round(comp_bytes / in_bytes, 5),
             "roundtrip_bit_exact": ok,
-            "roofline": {
-                "kernel": dom,
-                "bound": "hbm",
-                "achieved": round(achieved, 2),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBPS, 5),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": dom_bytes,
-                "avg_launch_ms": round(dom_ms, 4),
-            },
+            "all_roundtrips_bit_exact": ok_all,
+            "roofline": roofline(dom, kern[dom][1], kern[dom][0]),
+            "roofline_other": roofline(*[(k, v[1], v[0]) for k, v in kern.items() if k != dom][0]),
+            "random": rnd,
+            "large": large,
             "cpu_baseline": cpu,
         }
         line.update(extras)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
-    if not ok:
+    if not ok_all:
         sys.exit(3)
+
+
+def extra_modes(sm, batch, in_bytes):
+    """--extras: dense and reference (byte-identical) modes, validation."""
+    import torch
+    out = {}
+    t_dc = kernel_ms(lambda: batch.compress(sm, "dense"), 5)
+    out["dense_compress_GBps"] = round(in_bytes / (t_dc * 1e-3) / 1e9, 3)
+    out["dense_ratio"] = round(batch.comp_bytes() / in_bytes, 5)
+    t_dd = kernel_ms(lambda: batch.uncompress(sm), 5)
+    out["dense_streams_uncompress_GBps"] = round(in_bytes / (t_dd * 1e-3) / 1e9, 3)
+    out["dense_ok"] = batch.verify()
+    batch.compress(sm, "fast")
+    vst = torch.full_like(batch.status, -1)
+    t_v = kernel_ms(lambda: sm.validate_batch_device(batch.d_comp, batch.comp_off, batch.comp_len, vst), 5)
+    out["validate_GBps"] = round(in_bytes / (t_v * 1e-3) / 1e9, 3)
+    out["validate_ok"] = int(vst.abs().sum()) == 0
+    t_ref = kernel_ms(lambda: batch.compress(sm, "reference"), 3)
+    out["reference_mode_compress_GBps"] = round(in_bytes / (t_ref * 1e-3) / 1e9, 3)
+    out["reference_ratio"] = round(batch.comp_bytes() / in_bytes, 5)
+    t_rd3 = kernel_ms(lambda: batch.uncompress(sm), 5)
+    out["reference_streams_uncompress_GBps"] = round(in_bytes / (t_rd3 * 1e-3) / 1e9, 3)
+    out["reference_ok"] = batch.verify()
+    batch.compress(sm, "fast")
+    return out
 
 
 if __name__ == "__main__":

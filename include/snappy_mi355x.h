@@ -20,8 +20,9 @@
  *                         smaller output, about 10% slower.
  * Decompression has one mode, with the reference's accept/reject behaviour.
  *
- * Threading: an sm_ctx owns one HIP device, one stream and its scratch; calls on one ctx
- * must be serialised by the caller; distinct ctxs are independent.
+ * Threading: an sm_ctx owns one HIP device, one stream and its scratch.  The host-buffer
+ * entry points lock the ctx (concurrent callers on one ctx are serialised); the *_device entry
+ * points only launch on the caller's stream and take no lock.  Distinct ctxs are independent.
  */
 #ifndef SNAPPY_MI355X_H_
 #define SNAPPY_MI355X_H_
@@ -111,6 +112,15 @@ sm_status sm_compress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const u
                                        const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                        const uint64_t* d_out_off, uint32_t* d_out_len, uint64_t total_len,
                                        int mode, void* stream);
+/* Fragments of ONE stream, decoded (the inverse of sm_compress_fragments_device; the block loop
+ * of src/Snappy.jl:46-52 over src/internal.jl:411-466 without the varint header): fragment b is
+ * d_in[d_in_off[b] .. +d_in_len[b]) and must decode to exactly d_frag_len[b] (<= 65536) bytes at
+ * d_out + d_out_off[b].  d_status[b] / d_out_len[b] as in sm_uncompress_batch_device. */
+sm_status sm_uncompress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                         const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
+                                         const uint64_t* d_out_off, const uint32_t* d_frag_len, uint32_t* d_out_len,
+                                         int32_t* d_status, void* stream);
+
 /* Block b: compressed stream d_in[d_in_off[b] .. +d_in_len[b]) -> d_out + d_out_off[b] with
  * capacity d_out_cap[b].  d_status[b] = SM_OK or the reference's error code (first error in
  * stream order); d_out_len[b] = decoded bytes (0 on error).  Each block decodes as
@@ -154,6 +164,22 @@ sm_status sm_uncompress_batch_sharded(sm_ctx* const* ctxs, int nctx, const uint8
 /* snappy_validate_compressed_buffer (snappy-c.h) for one host buffer, on the device: the status
  * sm_uncompress would return with enough output room, without decoding into memory. */
 sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, size_t compressed_length);
+
+/* ---- snappy-c.h-shaped entry points, no ctx (a process-wide default context) ---------
+ * Same argument shapes and status meaning as libsnappy's snappy-c.h, i.e. exactly the ccall
+ * signature the reference's helper binds (test/libsnappy.jl:5-30:
+ * (Ptr{UInt8}, Csize_t, Ptr{UInt8}, Ref{Csize_t}) -> Cint), so a Julia binding switches from
+ * libsnappy by library and symbol name alone.  The default context is created on first use on
+ * device $SNAPPY_MI355X_DEVICE (default 0); calls are serialised on it.
+ * sm_snappy_compress uses SM_MODE_FAST unless sm_snappy_set_mode() selects another mode
+ * (SM_MODE_REFERENCE for Snappy.jl's exact bytes). */
+sm_status sm_snappy_compress(const char* input, size_t input_length, char* compressed, size_t* compressed_length);
+sm_status sm_snappy_uncompress(const char* compressed, size_t compressed_length, char* uncompressed,
+                               size_t* uncompressed_length);
+size_t sm_snappy_max_compressed_length(size_t source_length);
+sm_status sm_snappy_uncompressed_length(const char* compressed, size_t compressed_length, size_t* result);
+sm_status sm_snappy_validate_compressed_buffer(const char* compressed, size_t compressed_length);
+sm_status sm_snappy_set_mode(int mode);
 
 /* library build identification ("snappy_mi355x gfx950 <git-describe>") */
 const char* sm_version(void);

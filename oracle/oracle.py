@@ -172,3 +172,43 @@ def uncompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, status
     return lib().smo_uncompress_batch(inp.ctypes.data, in_off.ctypes.data, in_len.ctypes.data, in_len.size,
                                       out.ctypes.data, out_off.ctypes.data, out_cap.ctypes.data,
                                       out_len.ctypes.data, status.ctypes.data, nthreads)
+
+
+# ---- libsnappy (third-party comparison for the CPU baseline; not the oracle) ----------------
+
+LIBSNAPPY_PATH = "/opt/conda/lib/libsnappy.so.1"
+_lsb = None
+
+
+def libsnappy_batch():
+    """ctypes handle of liblibsnappy_batch.so with libsnappy dlopen'ed, or None when libsnappy
+    is absent on this host."""
+    global _lsb
+    if _lsb is None:
+        path = os.path.join(HERE, "liblibsnappy_batch.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.lsb_open.restype = ctypes.c_int
+        L.lsb_open.argtypes = [ctypes.c_char_p]
+        vp = ctypes.c_void_p
+        for fn in (L.lsb_compress_batch, L.lsb_uncompress_batch):
+            fn.restype = ctypes.c_int
+            fn.argtypes = [vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_int]
+        if not os.path.exists(LIBSNAPPY_PATH) or L.lsb_open(LIBSNAPPY_PATH.encode()) != 0:
+            _lsb = False
+        else:
+            _lsb = L
+    return _lsb or None
+
+
+def libsnappy_compress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, nthreads=1):
+    return libsnappy_batch().lsb_compress_batch(inp.ctypes.data, in_off.ctypes.data, in_len.ctypes.data, in_len.size,
+                                                out.ctypes.data, out_off.ctypes.data, out_cap.ctypes.data,
+                                                out_len.ctypes.data, nthreads)
+
+
+def libsnappy_uncompress_batch(inp, in_off, in_len, out, out_off, out_cap, out_len, nthreads=1):
+    return libsnappy_batch().lsb_uncompress_batch(inp.ctypes.data, in_off.ctypes.data, in_len.ctypes.data,
+                                                  in_len.size, out.ctypes.data, out_off.ctypes.data,
+                                                  out_cap.ctypes.data, out_len.ctypes.data, nthreads)

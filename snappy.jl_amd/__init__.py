@@ -10,8 +10,9 @@ include/snappy_mi355x.h (libsnappy_mi355x.so, hand-written gfx950 HIP kernels).
     parse32(buf, off) / encode32(v)     src/varint.jl:12 / :46 (0-based offsets)
 
 Errors raise SnappyError carrying the reference's exact ErrorException message.
-`mode="reference"` (default) produces Snappy.jl's exact bytes; `mode="fast"` uses the
-wave-parallel parse (valid snappy, decodes bit-exactly, different bytes).
+`mode="fast"` (default) uses the wave-parallel parse (valid snappy that decodes bit-exactly
+under Snappy.jl's uncompress, different bytes); `mode="reference"` produces Snappy.jl's exact
+bytes; `mode="dense"` is the fast parse with two chain candidates (smaller, slower).
 
 Batched GPU path (the north-star hot path): compress_batch / uncompress_batch on host
 arrays, and compress_batch_device / uncompress_batch_device on torch tensors already
@@ -22,6 +23,7 @@ HIP library and a device, and raises if either is missing.
 """
 import ctypes
 import os
+import threading
 
 import numpy as np
 
@@ -42,6 +44,9 @@ ABI_SYMBOLS = (
     "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device", "sm_ctx_last_path",
     "sm_find_match_length", "sm_validate_batch_device", "sm_uncompressed_length_batch_device",
     "sm_validate_compressed_buffer", "sm_compress_batch_sharded", "sm_uncompress_batch_sharded",
+    "sm_uncompress_fragments_device", "sm_snappy_compress", "sm_snappy_uncompress",
+    "sm_snappy_max_compressed_length", "sm_snappy_uncompressed_length", "sm_snappy_validate_compressed_buffer",
+    "sm_snappy_set_mode",
 )
 
 
@@ -55,6 +60,7 @@ class SnappyError(Exception):
 
 _lib = None
 _ctx = {}
+_ctx_lock = threading.Lock()
 
 
 def library_path():
@@ -115,6 +121,21 @@ def lib():
         L.sm_uncompressed_length_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
         L.sm_validate_compressed_buffer.restype = i32
         L.sm_validate_compressed_buffer.argtypes = [vp, vp, sz]
+        L.sm_uncompress_fragments_device.restype = i32
+        L.sm_uncompress_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+        # snappy-c.h shape (test/libsnappy.jl:5-30): (char*, size_t, char*, size_t*) -> int
+        L.sm_snappy_compress.restype = i32
+        L.sm_snappy_compress.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
+        L.sm_snappy_uncompress.restype = i32
+        L.sm_snappy_uncompress.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
+        L.sm_snappy_max_compressed_length.restype = sz
+        L.sm_snappy_max_compressed_length.argtypes = [sz]
+        L.sm_snappy_uncompressed_length.restype = i32
+        L.sm_snappy_uncompressed_length.argtypes = [vp, sz, ctypes.POINTER(sz)]
+        L.sm_snappy_validate_compressed_buffer.restype = i32
+        L.sm_snappy_validate_compressed_buffer.argtypes = [vp, sz]
+        L.sm_snappy_set_mode.restype = i32
+        L.sm_snappy_set_mode.argtypes = [ctypes.c_int]
         _lib = L
     return _lib
 
@@ -133,24 +154,27 @@ def _bytes(x):
 
 
 def context(device=0):
-    """Per-device sm_ctx (one HIP stream + scratch).  Raises if no device is usable."""
-    c = _ctx.get(device)
-    if c is None:
-        c = lib().sm_ctx_create(device)
-        if not c:
-            raise SnappyError(32, "no usable HIP device %d for snappy_mi355x" % device)
-        _ctx[device] = c
+    """Per-device sm_ctx (one HIP stream + scratch; the library serialises host-buffer calls on
+    it).  Raises if no device is usable."""
+    with _ctx_lock:
+        c = _ctx.get(device)
+        if c is None:
+            c = lib().sm_ctx_create(device)
+            if not c:
+                raise SnappyError(32, "no usable HIP device %d for snappy_mi355x" % device)
+            _ctx[device] = c
     return c
 
 
 def contexts(devices):
     """One sm_ctx per entry of `devices` for the sharded calls; a device listed twice gets a
-    second context (its own stream), so the sharding also runs on one GPU."""
+    second context (its own stream), so the sharding also runs on one GPU.  These contexts are
+    separate from the single-call context(d) (the sharded call rejects a ctx listed twice)."""
     seen, out = {}, []
     for d in devices:
         k = seen.get(d, 0)
         seen[d] = k + 1
-        key = d if k == 0 else (d, k)
+        key = ("shard", d, k)
         c = _ctx.get(key)
         if c is None:
             c = lib().sm_ctx_create(d)
@@ -195,7 +219,7 @@ def length_uncompressed(data):
     return parse32(data, 0)
 
 
-def compress(data, mode="reference", device=0):
+def compress(data, mode="fast", device=0):
     """Snappy.jl:20-36 (and the String method :38), computed on the GPU."""
     src = _bytes(data)
     if src.size > 0xFFFFFFFF:
@@ -373,6 +397,18 @@ def uncompress_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_ca
     st = lib().sm_uncompress_batch_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len),
                                           d_in_len.numel(), _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
                                           _ptr(d_out_len), _ptr(d_status), ctypes.c_void_p(stream))
+    if st:
+        raise SnappyError(st)
+
+
+def uncompress_fragments_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_frag_len, d_out_len, d_status,
+                                stream=None, device=None):
+    """Fragments of ONE stream (no varint headers; sm_compress_fragments_device's output):
+    fragment b must decode to exactly d_frag_len[b] bytes at d_out + d_out_off[b]."""
+    dev = d_in.device.index if device is None else device
+    st = lib().sm_uncompress_fragments_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len),
+                                              d_in_len.numel(), _ptr(d_out), _ptr(d_out_off), _ptr(d_frag_len),
+                                              _ptr(d_out_len), _ptr(d_status), ctypes.c_void_p(_stream(stream, dev)))
     if st:
         raise SnappyError(st)
 

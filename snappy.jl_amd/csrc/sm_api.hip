@@ -7,6 +7,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -39,11 +41,33 @@ struct DevBuf {
   }
 };
 
+struct HostBuf {  // pinned host staging (one D2H transfer per batch call)
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = n < (1u << 20) ? (1u << 20) : n;
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
 struct sm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf in, out, out2, meta, idx;
+  DevBuf in, out, out2, meta, idx, gat;
+  HostBuf stage;
   int last_path = -1;  // sm_ctx_last_path
+  std::mutex mu;       // serialises the host-buffer entry points (they share the scratch above)
 };
 
 namespace {
@@ -202,10 +226,42 @@ sm_status run_shards(int nctx, F&& shard_fn) {
   return SM_OK;
 }
 
+// The blocks [d_src + src_off[b], +len[b]) of a device batch back to host + out_off[b]: one
+// gather launch packs them back to back in ctx->out2, one D2H transfer brings them into the
+// pinned staging buffer, and the host scatters them (instead of one small copy per block).
+// len: host copy of the lengths (0 = nothing to copy); d_len: the same on the device.
+sm_status gather_to_host(sm_ctx* ctx, const uint8_t* d_src, const uint64_t* d_src_off, const uint32_t* d_len,
+                         const uint32_t* len, uint32_t nblk, const uint64_t* out_off, uint8_t* host) {
+  hipStream_t s = ctx->stream;
+  std::vector<uint64_t> dst(nblk);
+  uint64_t total = 0;
+  for (uint32_t b = 0; b < nblk; ++b) {
+    dst[b] = total;
+    total += len[b];
+  }
+  if (total == 0) return SM_OK;
+  if (ctx->gat.ensure(8 * (size_t)nblk) != hipSuccess || ctx->out2.ensure(total + 16) != hipSuccess ||
+      ctx->stage.ensure(total) != hipSuccess)
+    return SM_ERR_DEVICE;
+  uint64_t* d_dst = (uint64_t*)ctx->gat.p;
+  if (hipMemcpyAsync(d_dst, dst.data(), 8 * (size_t)nblk, hipMemcpyHostToDevice, s) != hipSuccess) return SM_ERR_DEVICE;
+  if (sm::launch_gather(d_src, d_src_off, d_len, d_dst, (uint8_t*)ctx->out2.p, nblk, s) != hipSuccess)
+    return SM_ERR_DEVICE;
+  if (hipMemcpyAsync(ctx->stage.p, ctx->out2.p, total, hipMemcpyDeviceToHost, s) != hipSuccess) return SM_ERR_DEVICE;
+  if (hipStreamSynchronize(s) != hipSuccess) return SM_ERR_DEVICE;
+  const uint8_t* st = (const uint8_t*)ctx->stage.p;
+  for (uint32_t b = 0; b < nblk; ++b)
+    if (len[b]) memcpy(host + out_off[b], st + dst[b], len[b]);
+  return SM_OK;
+}
+
 bool valid_ctxs(sm_ctx* const* ctxs, int nctx) {
   if (!ctxs || nctx <= 0) return false;
-  for (int i = 0; i < nctx; ++i)
+  for (int i = 0; i < nctx; ++i) {
     if (!ctxs[i]) return false;
+    for (int j = 0; j < i; ++j)
+      if (ctxs[j] == ctxs[i]) return false;  // two shards on one ctx would race on its scratch
+  }
   return true;
 }
 }  // namespace
@@ -331,6 +387,8 @@ void sm_ctx_destroy(sm_ctx* ctx) {
     ctx->out2.release();
     ctx->meta.release();
     ctx->idx.release();
+    ctx->gat.release();
+    ctx->stage.release();
     (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -391,6 +449,7 @@ sm_status sm_compress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_o
     if (ie > in_total) in_total = ie;
     if (oe > out_total) out_total = oe;
   }
+  std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
   size_t meta_bytes = (size_t)nblk * (8 + 4 + 8 + 4);
@@ -412,11 +471,7 @@ sm_status sm_compress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_o
   SM_CHECK(hipMemcpyAsync(out_len, d_out_len, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
   SM_CHECK(hipStreamSynchronize(s));
   // copy back only each block's bytes
-  for (uint32_t b = 0; b < nblk; ++b)
-    SM_CHECK(hipMemcpyAsync(out + out_off[b], (uint8_t*)ctx->out.p + out_off[b], out_len[b],
-                            hipMemcpyDeviceToHost, s));
-  SM_CHECK(hipStreamSynchronize(s));
-  return SM_OK;
+  return gather_to_host(ctx, (const uint8_t*)ctx->out.p, d_out_off, d_out_len, out_len, nblk, out_off, out);
 }
 
 sm_status sm_uncompress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
@@ -432,6 +487,7 @@ sm_status sm_uncompress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in
     if (ie > in_total) in_total = ie;
     if (oe > out_total) out_total = oe;
   }
+  std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
   size_t meta_bytes = (size_t)nblk * (8 + 8 + 4 + 4 + 4 + 4);
@@ -457,11 +513,8 @@ sm_status sm_uncompress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in
   SM_CHECK(hipMemcpyAsync(status, d_status, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
   SM_CHECK(hipStreamSynchronize(s));
   for (uint32_t b = 0; b < nblk; ++b)
-    if (status[b] == SM_OK && out_len[b])
-      SM_CHECK(hipMemcpyAsync(out + out_off[b], (uint8_t*)ctx->out.p + out_off[b], out_len[b],
-                              hipMemcpyDeviceToHost, s));
-  SM_CHECK(hipStreamSynchronize(s));
-  return SM_OK;
+    if (status[b] != SM_OK) out_len[b] = 0;  // (the kernel already reports 0 for failed blocks)
+  return gather_to_host(ctx, (const uint8_t*)ctx->out.p, d_out_off, d_out_len, out_len, nblk, out_off, out);
 }
 
 sm_status sm_validate_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
@@ -520,6 +573,7 @@ sm_status sm_uncompress_batch_sharded(sm_ctx* const* ctxs, int nctx, const uint8
 sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, size_t n) {
   if (!ctx || (n && !compressed)) return SM_ERR_ARGUMENT;
   if (n > 0xffffffffull) return SM_ERR_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
   SM_CHECK(ctx->in.ensure(n + 16));
@@ -566,6 +620,7 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
     in_len[i] = (uint32_t)((e < n ? e : n) - in_off[i]);
     out_off[i] = (uint64_t)i * slot;
   }
+  std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
   SM_CHECK(ctx->in.ensure(n + 16));
@@ -613,6 +668,7 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   if (n > 0xffffffffull) return SM_ERR_ARGUMENT;
   if (*uncompressed_length < size) return SM_BUFFER_TOO_SMALL;
   if (size && !uncompressed) return SM_ERR_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
   DeviceGuard g(ctx->device);
   hipStream_t s = ctx->stream;
   SM_CHECK(ctx->in.ensure(n + 16));
@@ -660,6 +716,72 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   }
   *uncompressed_length = dlen;
   return SM_OK;
+}
+
+sm_status sm_uncompress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
+                                         const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
+                                         const uint64_t* d_out_off, const uint32_t* d_frag_len, uint32_t* d_out_len,
+                                         int32_t* d_status, void* stream) {
+  if (!ctx) return SM_ERR_ARGUMENT;
+  if (nblk == 0) return SM_OK;
+  if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_frag_len || !d_out_len || !d_status)
+    return SM_ERR_ARGUMENT;
+  DeviceGuard g(ctx->device);
+  sm::DecompressArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_frag_len, d_out_len, d_status, nblk, 1};
+  SM_CHECK(sm::launch_decompress(a, 0, (hipStream_t)stream));
+  return SM_OK;
+}
+
+// ---- snappy-c.h-shaped entry points on a process-wide default context --------------------
+// The exact ccall shape of the reference's libsnappy helper (test/libsnappy.jl:5-30):
+// (Ptr{UInt8}, Csize_t, Ptr{UInt8}, Ref{Csize_t}) -> Cint, so a binding rebinds by symbol name
+// alone.  The default context lives on device SNAPPY_MI355X_DEVICE (default 0); its mutex
+// serialises callers.
+
+namespace {
+std::mutex g_default_mu;
+sm_ctx* g_default_ctx = nullptr;
+int g_default_mode = SM_MODE_FAST;
+
+sm_ctx* default_ctx() {
+  std::lock_guard<std::mutex> lk(g_default_mu);
+  if (!g_default_ctx) {
+    const char* e = getenv("SNAPPY_MI355X_DEVICE");
+    g_default_ctx = sm_ctx_create(e ? atoi(e) : 0);
+  }
+  return g_default_ctx;
+}
+}  // namespace
+
+sm_status sm_snappy_set_mode(int mode) {
+  if (!valid_mode(mode)) return SM_ERR_ARGUMENT;
+  g_default_mode = mode;
+  return SM_OK;
+}
+
+sm_status sm_snappy_compress(const char* input, size_t input_length, char* compressed, size_t* compressed_length) {
+  sm_ctx* ctx = default_ctx();
+  if (!ctx) return SM_ERR_DEVICE;
+  return sm_compress(ctx, input, input_length, compressed, compressed_length, g_default_mode);
+}
+
+sm_status sm_snappy_uncompress(const char* compressed, size_t compressed_length, char* uncompressed,
+                               size_t* uncompressed_length) {
+  sm_ctx* ctx = default_ctx();
+  if (!ctx) return SM_ERR_DEVICE;
+  return sm_uncompress(ctx, compressed, compressed_length, uncompressed, uncompressed_length);
+}
+
+size_t sm_snappy_max_compressed_length(size_t source_length) { return sm_max_compressed_length(source_length); }
+
+sm_status sm_snappy_uncompressed_length(const char* compressed, size_t compressed_length, size_t* result) {
+  return sm_uncompressed_length(compressed, compressed_length, result);
+}
+
+sm_status sm_snappy_validate_compressed_buffer(const char* compressed, size_t compressed_length) {
+  sm_ctx* ctx = default_ctx();
+  if (!ctx) return SM_ERR_DEVICE;
+  return sm_validate_compressed_buffer(ctx, compressed, compressed_length);
 }
 
 }  // extern "C"

@@ -597,8 +597,8 @@ __global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a)
   uint8_t* dst = a.out + a.out_off[b];
   const uint32_t cap = a.out_cap[b];
 
-  uint32_t size = 0, ip = 0;
-  int32_t st = parse_header(in, N, lane, size, ip);
+  uint32_t size = cap, ip = 0;
+  int32_t st = a.raw ? kOk : parse_header(in, N, lane, size, ip);
   if (st == kOk && size > cap) st = kBufferTooSmall;
   if (st == kOk) {
     uint32_t op_end = 0;

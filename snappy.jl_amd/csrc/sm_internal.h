@@ -30,6 +30,7 @@ struct DecompressArgs {
   uint32_t* out_len;
   int32_t* status;
   uint32_t nblk;
+  int raw;  // 1: no varint header -- a fragment of one stream, declared length = out_cap[b]
 };
 
 // mode 0 = reference (byte-identical to Snappy.jl), 1 = fast (wave-parallel parse), 2 = fast, denser

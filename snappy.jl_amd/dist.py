@@ -66,6 +66,16 @@ def gather_sizes(local_sizes, group=None):
     return torch.cat([p[:c] for p, c in zip(parts, counts)])
 
 
+def collective_device(group=None):
+    """Where a collective's tensors must live: the current GPU under nccl (RCCL), the CPU under
+    gloo."""
+    import torch
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device("cpu")
+
+
 def compress_stream_sharded(data, rank, world, compress_fn, group=None):
     """Compress one stream `data` (bytes) across `world` ranks.
 
@@ -78,8 +88,8 @@ def compress_stream_sharded(data, rank, world, compress_fn, group=None):
     lo, hi = shard_range(len(offs), rank, world)
     frags = [data[int(o): int(o) + int(l)] for o, l in zip(offs[lo:hi], lens[lo:hi])]
     out = compress_fn(frags, total) if frags else []
-    local = torch.tensor([len(x) for x in out], dtype=torch.int64)
-    sizes = gather_sizes(local, group).numpy()
+    local = torch.tensor([len(x) for x in out], dtype=torch.int64, device=collective_device(group))
+    sizes = gather_sizes(local, group).cpu().numpy()
     header = varint32(total)
     starts = len(header) + np.concatenate([[0], np.cumsum(sizes)[:-1]]) if len(sizes) else np.zeros(0, np.int64)
     return header, out, starts[lo:hi], int(len(header) + sizes.sum())
@@ -92,3 +102,31 @@ def assemble(header, pieces_with_offsets, total_len):
     for off, piece in pieces_with_offsets:
         buf[int(off): int(off) + len(piece)] = piece
     return bytes(buf)
+
+
+def stream_offsets_device(local_sizes, total_len, rank, world, group=None):
+    """Device-side global index of a stream sharded by `shard_range` (config 5): all-gather the
+    ranks' u32 fragment sizes (the only collective on the path; RCCL under nccl), then the
+    exclusive scan behind the varint(total_len) header.  local_sizes: this rank's fragment
+    sizes on the collective device.  Shard sizes are static (shard_range), so there is no host
+    round trip: every rank pads to the largest shard.  Returns (global offsets of this rank's
+    fragments, the stream's total length as a 1-element tensor) on local_sizes' device."""
+    import torch
+    import torch.distributed as dist
+    nfrag = (total_len + BLOCK - 1) // BLOCK
+    bounds = [shard_range(nfrag, r, world) for r in range(world)]
+    m = max(hi - lo for lo, hi in bounds)
+    dev = local_sizes.device
+    if world == 1:
+        sizes = local_sizes.to(torch.int64)
+    else:
+        buf = torch.zeros(m, dtype=torch.int64, device=dev)
+        buf[: local_sizes.numel()] = local_sizes.to(torch.int64)
+        parts = [torch.empty_like(buf) for _ in range(world)]
+        dist.all_gather(parts, buf, group=group)
+        sizes = torch.cat([p[: hi - lo] for p, (lo, hi) in zip(parts, bounds)])
+    hl = len(varint32(total_len))
+    incl = torch.cumsum(sizes, 0)
+    starts = hl + incl - sizes
+    lo, hi = bounds[rank]
+    return starts[lo:hi], incl[-1:] + hl

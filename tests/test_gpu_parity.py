@@ -34,7 +34,7 @@ def corpus():
 @pytest.mark.parametrize("fname", sorted(GOLDEN["corpus"]))
 def test_reference_mode_whole_file_matches_golden(sm, gpu_available, fname):
     raw = read_testfile(fname)
-    out = sm.compress(raw)                      # Snappy.jl compress(), multi-fragment, Q2 table
+    out = sm.compress(raw, mode="reference")  # Snappy.jl compress(), multi-fragment, Q2 table
     g = GOLDEN["corpus"][fname]
     assert len(out) == g["c_reference"]
     assert hashlib.sha256(out).hexdigest() == g["sha256_reference"]
@@ -52,10 +52,10 @@ def test_reference_mode_batched_blocks(sm, oracle, gpu_available, corpus):
 def test_reference_mode_edge_strings(sm, oracle, gpu_available):
     from golden.make_golden import EDGE_STRINGS
     for s, g in zip(EDGE_STRINGS, GOLDEN["edge_strings"]):
-        out = sm.compress(s)
+        out = sm.compress(s, mode="reference")
         assert hashlib.sha256(out).hexdigest() == g["sha256_reference"]
         assert sm.uncompress(out) == s
-    assert sm.compress("abc") == bytes.fromhex("0308616263")      # String method, Snappy.jl:38
+    assert sm.compress("abc", mode="reference") == bytes.fromhex("0308616263")      # String method, Snappy.jl:38
 
 
 def test_reference_mode_small_sizes(sm, oracle, gpu_available):
@@ -80,7 +80,7 @@ def test_reference_mode_dictionary_streams(sm, oracle, gpu_available):
     rng = np.random.default_rng(0x5EED)
     for _ in range(6):
         raw = dictionary_stream(rng, 1 << 14)
-        assert sm.compress(raw) == oracle.compress(raw)
+        assert sm.compress(raw, mode="reference") == oracle.compress(raw)
 
 
 def test_reference_mode_fragments_device(sm, oracle, gpu_available):
