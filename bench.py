@@ -282,11 +282,40 @@ def roofline(kernel, alg_bytes, ms):
 
 # ---- CPU baseline ----------------------------------------------------------------------------
 
+def cpu_quota():
+    """CPUs the cgroup lets this process use (cgroup v2 cpu.max or v1 cfs quota), or None."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            if parse:
+                q, per = parse(open(path).read())
+                if q != "max":
+                    return max(1, int(int(q) / int(per)))
+            else:
+                q = int(open(path).read())
+                per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                if q > 0:
+                    return max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    return None
+
+
 def cpu_cores():
+    """Host threads for the CPU baseline: the CPUs this process may run on, capped by the cgroup
+    quota and by OMP_NUM_THREADS when set (the GPU box sets it to the job's CPU share, 16 of
+    the machine's 256; oversubscribing that share measured 0.9 GB/s instead of ~6)."""
     try:
-        return len(os.sched_getaffinity(0))
+        n = len(os.sched_getaffinity(0))
     except AttributeError:
-        return os.cpu_count() or 1
+        n = os.cpu_count() or 1
+    q = cpu_quota()
+    if q:
+        n = min(n, q)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return n
 
 
 def cpu_model():
@@ -342,9 +371,9 @@ def cpu_baseline(blocks_np, nblk=2048, reps=10, single_reps=3):
         "cores": threads,
         "kind": "port",
         "sample": "%d x 64 KiB text blocks (the first %d of the headline workload); reference-mode compress + "
-                  "uncompress by oracle/snappy_oracle.c (-O3, OpenMP over blocks on %d threads = every core this "
-                  "process may use; os.cpu_count() = %d, %s); median of %d passes" % (
-                      nblk, nblk, threads, os.cpu_count() or 0, cpu_model(), reps),
+                  "uncompress by oracle/snappy_oracle.c (-O3, OpenMP over blocks on %d threads = this job's CPU "
+                  "share (affinity, cgroup quota, OMP_NUM_THREADS); os.cpu_count() = %d, %s); median of %d "
+                  "passes" % (nblk, nblk, threads, os.cpu_count() or 0, cpu_model(), reps),
         "compress_GBps": round(c_all, 4),
         "uncompress_GBps": round(d_all, 4),
         "single_thread_compress_GBps": round(c_one, 4),

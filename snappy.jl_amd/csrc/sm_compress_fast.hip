@@ -36,6 +36,8 @@
 
 namespace sm {
 
+constexpr uint32_t kScreenTodo = 0xfffffffeu;  // out_len mark of k_literal_screen: the parse compresses this block
+
 #if SM_STAMP
 __device__ unsigned long long g_stamp_c[12];
 __device__ unsigned long long g_stamp_w[16];  // barrier wait per wave index
@@ -573,6 +575,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
                   (inserter ? 0 : wave) * kP;  // per-wave copy-start bitmask
 
   const uint32_t b = blockIdx.x;
+  if (a.screened && a.out_len[b] != kScreenTodo) return;  // emitted as one literal by k_literal_screen
   const uint32_t n = a.in_len[b];
   const uint8_t* src = a.in + a.in_off[b];
   uint8_t* dst = a.out + a.out_off[b];
@@ -743,14 +746,164 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 
 
 
+// ---- incompressible screen ---------------------------------------------------------------
+// Before the parse, one light workgroup per block samples kScrWin windows of kScrWB bytes spread
+// evenly over the block and counts the sample positions whose 4 bytes occurred earlier in the
+// sample.  Compressible data counts in the thousands (text 900-1700 of the 4,000 positions,
+// structured data 2,000-3,400); compressed, encrypted and random data counts 0-130 (jpeg,
+// the tail of a pdf, a snappy stream).  Below kScrMin the block is emitted here as ONE literal
+// (header, emit_literal! tag, the bytes: internal.jl:271-284 -- the reference's own output for
+// random 64 KiB blocks is also one 65,542-B literal), copied with aligned 16-B loads and stores
+// at HBM speed; the parse kernel then skips it.  This is the batch analogue of the reference's
+// skip heuristic (internal.jl:162-175), which stops looking for matches in data without them.
+// The bet only costs ratio, never validity: a literal encodes any bytes.
+constexpr uint32_t kScrWin = 32, kScrWB = 128;  // 4 KiB sample
+constexpr uint32_t kScrMin = 192;               // repeated sample positions that make a block "compressible"
+constexpr uint32_t kScrMinLen = 8192;           // smaller blocks always take the parse
+constexpr uint32_t kScrThreads = 256;
+constexpr uint32_t kScrTabBits = 12;
+
+__global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t samp[kScrWin * kScrWB + 16];
+  __shared__ uint32_t tab[1u << kScrTabBits];
+  __shared__ uint32_t cnt;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t b = blockIdx.x;
+  const uint32_t n = a.in_len[b];
+  const uint8_t* src = a.in + a.in_off[b];
+  uint8_t* dst = a.out + a.out_off[b];
+  if (n < kScrMinLen || n > kBlockSize) {
+    if (tid == 0) a.out_len[b] = kScreenTodo;
+    return;
+  }
+  // (1) the sample: window i at (i (n - WB) / (W - 1)) & ~15, one 16-B piece per thread
+  static_assert(kScrWin * kScrWB == 16 * kScrThreads, "one piece per thread");
+  {
+    const uint32_t w = tid / (kScrWB / 16), k = tid % (kScrWB / 16);
+    const uint32_t o = ((w * (n - kScrWB)) / (kScrWin - 1)) & ~15u;
+    const uint8_t* s = src + o + 16 * k;
+    uint4 v;
+    if (((uintptr_t)src & 15) == 0) {
+      v = *reinterpret_cast<const uint4*>(s);
+    } else {
+      uint32_t x[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        x[i] = (uint32_t)s[4 * i] | ((uint32_t)s[4 * i + 1] << 8) | ((uint32_t)s[4 * i + 2] << 16) |
+               ((uint32_t)s[4 * i + 3] << 24);
+      v = make_uint4(x[0], x[1], x[2], x[3]);
+    }
+    reinterpret_cast<uint4*>(samp)[tid] = v;
+  }
+  for (uint32_t k = tid; k < (1u << kScrTabBits); k += kScrThreads) tab[k] = 0xffffffffu;
+  if (tid == 0) cnt = 0;
+  if (tid < 4) reinterpret_cast<uint32_t*>(samp + kScrWin * kScrWB)[tid] = 0;
+  __syncthreads();
+  // (2) first occurrence of every sample 4-gram (atomic min), then the repeats
+  constexpr uint32_t kPer = kScrWin * kScrWB / kScrThreads;  // 16 positions per thread, strided by 256
+  uint32_t wv[kPer], hv[kPer];
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t p = tid + kScrThreads * i;
+    wv[i] = lds_ld32(samp, p);
+    hv[i] = (wv[i] * kHashMul) >> (32 - kScrTabBits);
+    if (p % kScrWB <= kScrWB - 4) atomicMin(&tab[hv[i]], p);
+  }
+  __syncthreads();
+  uint32_t mine = 0;
+#pragma unroll
+  for (uint32_t i = 0; i < kPer; ++i) {
+    const uint32_t p = tid + kScrThreads * i;
+    const uint32_t q = tab[hv[i]];
+    mine += (p % kScrWB <= kScrWB - 4 && q < p && lds_ld32(samp, q) == wv[i]) ? 1u : 0u;
+  }
+  const uint32_t wsum = __builtin_amdgcn_readlane(scan_dpp(mine), 63);
+  if (lane == 0) atomicAdd(&cnt, wsum);
+  __syncthreads();
+  if (cnt >= kScrMin) {
+    if (tid == 0) a.out_len[b] = kScreenTodo;
+    return;
+  }
+  // (3) literal-only stream: [varint n] + literal tag + the n bytes.  D[j] = src[j - h] for
+  // j >= h.  Destination 16-B units that lie inside [h, h + n) are assembled from two aligned
+  // source units (the second from the neighbouring lane, DPP) with one byte shift; the partial
+  // units at either end are written byte by byte.
+  const uint32_t hv0 = a.header ? varint_len(n) : 0u;
+  const uint32_t h = hv0 + literal_tag_bytes(n);
+  const uint32_t ad = (uint32_t)((uintptr_t)dst & 15), as = (uint32_t)((uintptr_t)src & 15);
+  // dst unit u covers D offsets [16u - ad, 16u - ad + 16); the source of its first byte is
+  // src-aligned offset 16u + e, e = as - ad - h
+  const int32_t e = (int32_t)as - (int32_t)ad - (int32_t)h;
+  const int32_t E = e >= 0 ? e / 16 : -((15 - e) / 16);  // floor(e / 16)
+  const uint32_t m = (uint32_t)(e - 16 * E);              // byte shift 0..15
+  const uint32_t u0 = (h + ad + 15) / 16;                 // first full unit
+  const uint32_t u1 = (h + n + ad) / 16;                  // one past the last full unit
+  const uint4* s16 = reinterpret_cast<const uint4*>(src - as);
+  uint4* d16 = reinterpret_cast<uint4*>(dst - ad);
+  const uint32_t send = as + n;  // src-aligned byte offset one past the block
+  for (uint32_t base = u0 + (tid & ~63u); base < u1; base += kScrThreads) {
+    const uint32_t u = base + lane;
+    const int32_t su = (int32_t)u + E;  // >= 0 for full units
+    uint4 lo = make_uint4(0, 0, 0, 0), hi;
+    if (u < u1) lo = s16[su];
+    // the next source unit: the next lane's lo, except in lane 63 and past u1
+    hi.x = __builtin_amdgcn_update_dpp(0u, lo.x, 0x130, 0xf, 0xf, false);
+    hi.y = __builtin_amdgcn_update_dpp(0u, lo.y, 0x130, 0xf, 0xf, false);
+    hi.z = __builtin_amdgcn_update_dpp(0u, lo.z, 0x130, 0xf, 0xf, false);
+    hi.w = __builtin_amdgcn_update_dpp(0u, lo.w, 0x130, 0xf, 0xf, false);
+    if ((lane == 63 || u + 1 >= u1) && u < u1 && m != 0 && 16u * (uint32_t)(su + 1) < send) hi = s16[su + 1];
+    if (u < u1) {
+      const uint32_t x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      const uint32_t dw = m >> 2, sb = m & 3u;
+      uint32_t r[5];
+#pragma unroll
+      for (int k = 0; k < 5; ++k) {  // x[dw + k], selects (no dynamic register indexing)
+        uint32_t v = x[k];
+#pragma unroll
+        for (int d = 1; d < 4; ++d) v = dw == (uint32_t)d ? x[k + d] : v;
+        r[k] = v;
+      }
+      uint4 o;
+      o.x = __builtin_amdgcn_alignbyte(r[1], r[0], sb);
+      o.y = __builtin_amdgcn_alignbyte(r[2], r[1], sb);
+      o.z = __builtin_amdgcn_alignbyte(r[3], r[2], sb);
+      o.w = __builtin_amdgcn_alignbyte(r[4], r[3], sb);
+      d16[u] = o;
+    }
+  }
+  // partial units: D offsets [0, 16 u0 - ad) and [16 u1 - ad, h + n), plus the header bytes
+  const uint32_t headEnd = min(16 * u0 - ad, h + n), tailBeg = max(16 * u1 - ad, headEnd);
+  const uint32_t nh = headEnd, nt = h + n - tailBeg;
+  for (uint32_t j = tid; j < nh + nt; j += kScrThreads) {
+    const uint32_t jj = j < nh ? j : tailBeg + (j - nh);
+    uint8_t v;
+    if (jj < hv0) {
+      v = (uint8_t)(((n >> (7 * jj)) & 0x7f) | (jj + 1 < hv0 ? 0x80 : 0));
+    } else if (jj < h) {  // emit_literal! tag: 60..63 << 2 then len-1 little-endian
+      const uint32_t tb = h - hv0, k = jj - hv0;
+      v = tb == 1 ? (uint8_t)((n - 1) << 2) : (k == 0 ? (uint8_t)((58 + tb) << 2) : (uint8_t)((n - 1) >> (8 * (k - 1))));
+    } else {
+      v = src[jj - h];
+    }
+    dst[jj] = v;
+  }
+  if (tid == 0) a.out_len[b] = h + n;
+}
+
 template <int D>
 static hipError_t launch_depth(const CompressArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_compress_fast<D>, dim3(a.nblk), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 
-// mode 1 (SM_MODE_FAST): one chain candidate per position; mode 2 (SM_MODE_FAST_DENSE): two
-hipError_t launch_compress_fast(const CompressArgs& a, int mode, hipStream_t s) {
+// mode 1 (SM_MODE_FAST): one chain candidate per position; mode 2 (SM_MODE_FAST_DENSE): two.
+// The screen runs first; the parse kernel compresses the blocks it marks kScreenTodo.
+hipError_t launch_compress_fast(const CompressArgs& a0, int mode, hipStream_t s) {
+  CompressArgs a = a0;
+  a.screened = 1;
+  hipLaunchKernelGGL(k_literal_screen, dim3(a.nblk), dim3(kScrThreads), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   return mode == 2 ? launch_depth<2>(a, s) : launch_depth<1>(a, s);
 }
 

@@ -18,6 +18,7 @@ struct CompressArgs {
   uint32_t nblk;
   uint32_t table_size;  // 0: per block from its length (internal.jl:107-113); else fixed (Q2)
   int header;           // 1: prefix each block with varint(len) (independent snappy stream)
+  int screened;         // set by launch_compress_fast: out_len holds k_literal_screen's verdicts
 };
 
 struct DecompressArgs {

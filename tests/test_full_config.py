@@ -100,8 +100,9 @@ def test_config4_random_full_batch(sm, oracle, gpu_available, random10k, mode):
     assert not gst.any() and np.array_equal(gdec, random10k.reshape(-1))
     odec, ost, _ = _oracle_decode(oracle, comp, clen, random10k.shape[0])
     assert not ost.any() and np.array_equal(odec, random10k.reshape(-1))
-    # literal-only: header (3 B) + literal tags; the reference emits 65,542 B per block
-    assert clen.max() <= 65536 + 3 + 3 * 4, clen.max()
+    # (nearly) literal-only: header + a few literal tags (and the odd chance match); the
+    # reference emits 65,542 B per block.  Bound: 0.1 % over the input.
+    assert clen.max() <= 65536 + 65, clen.max()
 
 
 def test_reference_mode_subset_byte_identical(sm, oracle, gpu_available, text10k):
