@@ -30,7 +30,8 @@
 #include "sm_device.h"
 #include "sm_internal.h"
 
-#ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches, 4 inserter only, 8 no extension past 8 bytes
+#ifndef SM_ABLATE  // diagnostic builds only: 1 no emit, 2 no matches, 4 inserter only, 8 no extension past 8 bytes,
+                   // 16 no global stores in the emission
 #define SM_ABLATE 0
 #endif
 
@@ -256,11 +257,12 @@ struct ChunkTok {
   uint64_t ts[kP];           // copy-start bitmask of the chunk's positions
 };
 
-// Parse of chunk [c0, ce) (ce > c0) from its ring candidates cr; returns the chunk info word
-// for the round layout: unmerged size | leading literal piece << 11 | trailing literal piece
-// << 20 | no copies at all << 29.
+// Parse of chunk [c0, ce) (ce > c0); returns the chunk info word for the round layout:
+// unmerged size | leading literal piece << 11 | trailing literal piece << 20 | no copies at all
+// << 29.  cvin[j]: the ring candidates of position c0 + 64j + lane, u16 halves of position + 1
+// (0: none); kDepth halves are verified.
 template <int kDepth>
-__device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<kDepth>::Cand* cr, uint8_t* jt, uint64_t* tsw,
+__device__ inline uint32_t parse_chunk(const uint8_t* data, const uint32_t (&cvin)[kP], uint8_t* jt, uint64_t* tsw,
                                        uint32_t c0, uint32_t ce, uint32_t n, uint32_t lane, ChunkTok& t) {
   t.c0 = c0;
   t.ce = ce;
@@ -278,7 +280,7 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const typename Cfg<k
 #pragma unroll
   for (int j = 0; j < kP; ++j) {
     const uint32_t q = c0 + 64 * j + lane;
-    cvs[j] = cr[64 * j + lane];
+    cvs[j] = cvin[j];
     wqs[j] = lds_ld64(data, q < n ? q : 0);  // the 8 bytes at q
   }
 #pragma unroll
@@ -516,7 +518,8 @@ __device__ inline void emit_chunk(uint8_t* dst, const uint8_t* data, const Chunk
     mytag = lit_tag_bytes(myrun);
     tagv = myrun;
   }
-  if (lane < t.ntok) {
+  const bool st_on = !(SM_ABLATE & 16) || dst == nullptr;  // ablation 16: no global stores (kept computation)
+  if (lane < t.ntok && st_on) {
     put_lit_tag(dst, o, mytag, tagv);
     if (tL) put_copy_cf(dst, o + mytag + t.litlen, t.tb, tL);
   }
@@ -542,8 +545,60 @@ __device__ inline void emit_chunk(uint8_t* dst, const uint8_t* data, const Chunk
     const uint32_t x = t.c0 + 64 * j + lane;
     // one mask (bitwise, so the compiler does not split it into nested branches)
     const bool lit = (x < t.ce) & ((cnt[j] == 0) | (x >= pend[j]));
-    if (lit) dst[x + dl[j]] = (uint8_t)v[j];  // 32-bit offset: saddr store
+    if (lit && st_on) dst[x + dl[j]] = (uint8_t)v[j];  // 32-bit offset: saddr store
   }
+}
+
+// Round layout, lane-parallel over the round's chunk slots (lane u = slot u): a literal run
+// that crosses chunk boundaries inside the round is emitted once, with one tag for its total
+// length in the chunk where it starts (runs restart at round boundaries).
+//   cont_in[u]: chunk u's leading literal piece continues chunk u-1's trailing piece (no tag)
+//   mid[u]:     chunk u is all literal and continues a run (no tag of its own)
+//   start[u]:   chunk u's trailing piece starts a run; if cont_in[u+1] the run spans chunks
+//               and its tag encodes the run length up to the end of the last piece.
+struct RoundLayout {
+  uint32_t inclm, Smv, contv, runv, total;
+};
+template <uint32_t kSlots>
+__device__ inline RoundLayout round_layout(const uint32_t* cinfo, uint32_t r, uint32_t n, uint32_t lane) {
+  uint32_t inclm, Smv, contv, runv, total;
+  const uint32_t info = lane < kSlots ? cinfo[lane] : 0u;
+  const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0x1ffu, trl = (info >> 20) & 0x1ffu;
+  const bool nocp = (info >> 29) & 1u;
+  const uint32_t trl_prev = __builtin_amdgcn_update_dpp(0u, trl, 0x138, 0xf, 0xf, false);  // wave_shr:1
+  const bool cont_in = lane > 0 && lane < kSlots && trl_prev > 0 && lead > 0;
+  const bool mid = nocp && cont_in;
+  const bool start = trl > 0 && !mid;
+  const bool cont_next = __builtin_amdgcn_update_dpp(0u, (uint32_t)cont_in, 0x130, 0xf, 0xf, false) != 0;  // wave_shl:1
+  const uint32_t cu = (r * kSlots + lane) * kChunk;                      // chunk start
+  const uint32_t ceu = min(cu + kChunk, n);
+  // the run ending in chunk u ends at cu + lead; a run starting in chunk v ends in the
+  // first later chunk whose piece ends it (suffix min over lanes)
+  const bool ends = cont_in && !(mid && cont_next);
+  uint32_t nxt = ends ? lane : 0xffu;
+  if (kSlots < 16) {  // one DPP row
+    nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x101, 0xf, 0xf, false));  // row_shl:1
+    nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x102, 0xf, 0xf, false));  // row_shl:2
+    nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x104, 0xf, 0xf, false));  // row_shl:4
+    nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x108, 0xf, 0xf, false));  // row_shl:8
+  } else {
+#pragma unroll
+    for (uint32_t d = 1; d < kSlots; d <<= 1) {
+      const uint32_t o2 = __shfl_down(nxt, d, 64);
+      nxt = (lane + d < kSlots && o2 < nxt) ? o2 : nxt;
+    }
+  }
+  nxt = __builtin_amdgcn_update_dpp(0xffu, nxt, 0x130, 0xf, 0xf, false);                       // first end after u
+  const uint32_t endpos = __shfl(cu + lead, nxt & 63u, 64);
+  const uint32_t runlen = (start && cont_next) ? endpos - (ceu - trl) : 0u;
+  const uint32_t Sm = S - (cont_in ? lit_tag_bytes(lead) : 0u) +
+                      (runlen ? lit_tag_bytes(runlen) - lit_tag_bytes(trl) : 0u);
+  inclm = scan_dpp(lane < kSlots ? Sm : 0u);
+  total = readlane(inclm, kSlots - 1);
+  Smv = Sm;
+  contv = cont_in;
+  runv = runlen;
+  return RoundLayout{inclm, Smv, contv, runv, total};
 }
 
 template <int D>
@@ -647,8 +702,11 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         if (SM_FAST_PPRIO && u == 1) __builtin_amdgcn_s_setprio(0);
         if (k < nchunks && !(SM_ABLATE & 4)) {
           STAMP_COUNT(11, 1)
-          const uint32_t info = parse_chunk<kDepth>(data, ring + (r & 1) * kRP + slot * kChunk, jt, tsw, c0,
-                                                    min(c0 + kChunk, n), n, lane, tk[u]);
+          const Cand* cr = ring + (r & 1) * kRP + slot * kChunk;
+          uint32_t cv[kP];
+#pragma unroll
+          for (int j = 0; j < kP; ++j) cv[j] = cr[64 * j + lane];
+          const uint32_t info = parse_chunk<kDepth>(data, cv, jt, tsw, c0, min(c0 + kChunk, n), n, lane, tk[u]);
           if (lane == 0) cinfo[slot] = info;
         } else {
           tk[u].c0 = tk[u].ce = c0;
@@ -665,52 +723,9 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     STAMP(4)
     if (SM_FAST_PPRIO) __builtin_amdgcn_s_setprio(2);
 
-    // (c) round layout, lane-parallel over the round's chunks (lane u = chunk slot u): a
-    // literal run that crosses chunk boundaries inside the round is emitted once, with one
-    // tag for its total length in the chunk where it starts (runs restart at round boundaries).
-    //   cont_in[u]: chunk u's leading literal piece continues chunk u-1's trailing piece (no tag)
-    //   mid[u]:     chunk u is all literal and continues a run (no tag of its own)
-    //   start[u]:   chunk u's trailing piece starts a run; if cont_in[u+1] the run spans chunks
-    //               and its tag encodes the run length up to the end of the last piece.
-    uint32_t inclm, Smv, contv, runv, total;
-    {
-      const uint32_t info = lane < kSlots ? cinfo[lane] : 0u;
-      const uint32_t S = info & 0x7ffu, lead = (info >> 11) & 0x1ffu, trl = (info >> 20) & 0x1ffu;
-      const bool nocp = (info >> 29) & 1u;
-      const uint32_t trl_prev = __builtin_amdgcn_update_dpp(0u, trl, 0x138, 0xf, 0xf, false);  // wave_shr:1
-      const bool cont_in = lane > 0 && lane < kSlots && trl_prev > 0 && lead > 0;
-      const bool mid = nocp && cont_in;
-      const bool start = trl > 0 && !mid;
-      const bool cont_next = __builtin_amdgcn_update_dpp(0u, (uint32_t)cont_in, 0x130, 0xf, 0xf, false) != 0;  // wave_shl:1
-      const uint32_t cu = (r * kSlots + lane) * kChunk;                      // chunk start
-      const uint32_t ceu = min(cu + kChunk, n);
-      // the run ending in chunk u ends at cu + lead; a run starting in chunk v ends in the
-      // first later chunk whose piece ends it (suffix min over lanes)
-      const bool ends = cont_in && !(mid && cont_next);
-      uint32_t nxt = ends ? lane : 0xffu;
-      if (kSlots < 16) {  // one DPP row
-        nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x101, 0xf, 0xf, false));  // row_shl:1
-        nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x102, 0xf, 0xf, false));  // row_shl:2
-        nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x104, 0xf, 0xf, false));  // row_shl:4
-        nxt = min(nxt, (uint32_t)__builtin_amdgcn_update_dpp(0xffu, nxt, 0x108, 0xf, 0xf, false));  // row_shl:8
-      } else {
-#pragma unroll
-        for (uint32_t d = 1; d < kSlots; d <<= 1) {
-          const uint32_t o2 = __shfl_down(nxt, d, 64);
-          nxt = (lane + d < kSlots && o2 < nxt) ? o2 : nxt;
-        }
-      }
-      nxt = __builtin_amdgcn_update_dpp(0xffu, nxt, 0x130, 0xf, 0xf, false);                       // first end after u
-      const uint32_t endpos = __shfl(cu + lead, nxt & 63u, 64);
-      const uint32_t runlen = (start && cont_next) ? endpos - (ceu - trl) : 0u;
-      const uint32_t Sm = S - (cont_in ? lit_tag_bytes(lead) : 0u) +
-                          (runlen ? lit_tag_bytes(runlen) - lit_tag_bytes(trl) : 0u);
-      inclm = scan_dpp(lane < kSlots ? Sm : 0u);
-      total = readlane(inclm, kSlots - 1);
-      Smv = Sm;
-      contv = cont_in;
-      runv = runlen;
-    }
+    // (c) round layout (round_layout), then the emission
+    const RoundLayout lay = round_layout<kSlots>(cinfo, r, n, lane);
+    const uint32_t inclm = lay.inclm, Smv = lay.Smv, contv = lay.contv, runv = lay.runv, total = lay.total;
     STAMP(5)
     if (!(SM_ABLATE & 1)) {
 #pragma unroll
