@@ -273,9 +273,21 @@ def pmc_traffic(kernel):
         return None
 
 
+# the rocprof kernels behind each timed call (a fast-mode compress is the incompressible screen
+# then the parse; avg_launch_ms is their sum, HIP events around the call)
+ROCPROF_KERNELS = {
+    "compress_fast": ["sm::k_literal_screen", "sm::k_compress_fast<1>"],
+    "compress_fast_random": ["sm::k_literal_screen", "sm::k_compress_fast<1>"],
+    "compress_fragments": ["sm::k_literal_screen", "sm::k_compress_fast<1>"],
+    "uncompress": ["sm::k_decompress"],
+    "uncompress_random": ["sm::k_decompress"],
+}
+
+
 def roofline(kernel, alg_bytes, ms):
     achieved = alg_bytes / (ms * 1e-3) / 1e9
-    return {"kernel": kernel, "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+    return {"kernel": kernel, "rocprof_kernels": ROCPROF_KERNELS.get(kernel), "bound": "hbm",
+            "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": pmc_traffic(kernel),
             "algorithmic_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4)}
 

@@ -24,7 +24,7 @@ def main():
     args = ap.parse_args()
     sm = bench.load_package()
     dev = torch.device("cuda", 0)
-    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 7)
+    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 0x5EED + 1)
     b = bench.Batch(blocks, dev)
     b.compress(sm, "fast")
     torch.cuda.synchronize()

@@ -17,26 +17,34 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import summarise  # noqa: E402
 
-KERNELS = {"compress_fast": ("pmc_compress", "k_compress_fast"),
-           "uncompress": ("pmc_uncompress", "k_decompress")}
+# bench.py roofline key -> (pass directory, rocprof kernel names summed per launch).  A fast-mode
+# compress call is two kernels: the incompressible screen and the parse (which returns at once
+# for the blocks the screen emitted).
+KERNELS = {"compress_fast": ("pmc_compress", ["k_literal_screen", "k_compress_fast<1>"]),
+           "uncompress": ("pmc_uncompress", ["k_decompress("]),
+           "compress_fast_random": ("pmc_compress_random", ["k_literal_screen", "k_compress_fast<1>"]),
+           "uncompress_random": ("pmc_uncompress_random", ["k_decompress("])}
 
 
 def main(root, out_path):
     res = {"source": "rocprofv3 --kernel-trace --pmc, one pass per counter group (tools/pmc_run.sh)",
-           "units": "bytes per launch (10000 x 64 KiB text blocks)"}
-    for key, (sub, kname) in KERNELS.items():
-        d = summarise(os.path.join(root, sub), kname)
-        if not d:
+           "units": "bytes per launch (10000 x 64 KiB blocks: text, or uniform random for *_random)"}
+    for key, (sub, knames) in KERNELS.items():
+        per = {}
+        for kn in knames:
+            d = summarise(os.path.join(root, sub), kn)
+            if d:
+                per[next(iter(d.keys()))] = next(iter(d.values()))
+        if not per:
             continue
-        ctr = next(iter(d.values()))
-        fetch = ctr.get("FETCH_SIZE", 0.0) * 1024.0
-        write = ctr.get("WRITE_SIZE", 0.0) * 1024.0
+        fetch = sum(c.get("FETCH_SIZE", 0.0) for c in per.values()) * 1024.0
+        write = sum(c.get("WRITE_SIZE", 0.0) for c in per.values()) * 1024.0
         res[key] = {
-            "kernel": next(iter(d.keys()))[:60],
+            "kernels": [k[:60] for k in per],
             "fetch_size_bytes_raw": fetch,
             "write_size_bytes": write,
             "hbm_bytes_per_launch": 2.0 * fetch + write,
-            "counters": {k: v for k, v in sorted(ctr.items())},
+            "counters": {k[:60]: {n: v for n, v in sorted(c.items())} for k, c in per.items()},
         }
     json.dump(res, open(out_path, "w"), indent=1)
     print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in res.items() if isinstance(v, dict)}))

@@ -42,7 +42,7 @@ def main():
     fn = lib.sm_debug_stamps
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     dev = torch.device("cuda", 0)
-    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 7)
+    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 0x5EED + 1)
     b = bench.Batch(blocks, dev)
     b.compress(sm, "fast")
     b.uncompress(sm)
@@ -71,7 +71,7 @@ def compress_stamps(args):
     fn = sm.lib().sm_debug_stamps_c
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     dev = torch.device("cuda", 0)
-    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 7)
+    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 0x5EED + 1)
     b = bench.Batch(blocks, dev)
     b.compress(sm, "fast")
     torch.cuda.synchronize()
@@ -104,7 +104,7 @@ def exact_stamps(args):
     fn = sm.lib().sm_debug_stamps_x
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
     dev = torch.device("cuda", 0)
-    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 7)
+    blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 0x5EED + 1)
     b = bench.Batch(blocks, dev)
     buf = (ctypes.c_ulonglong * 8)()
     b.compress(sm, "reference")
