@@ -227,23 +227,24 @@ def load_package_cached():
 
 
 def timed_steps(step, steps, warmup, world, dist, dev):
+    # dist is None unless a process group is up (world > 1, or SM_BENCH_DIST=1)
     """W untimed steps, then K steps between barrier + synchronize on both sides; max over ranks."""
     import torch
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -471,10 +472,24 @@ def main():
         print("bench.py: rank %d needs GPU %d but %d visible" % (rank, local_rank, ndev), file=sys.stderr)
         sys.exit(2)
     dist = None
-    if world > 1:
+    # SM_BENCH_DIST=1 (diagnostic): run the RCCL code path (process group, size all-gather,
+    # barriers, max-over-ranks) even at one rank, to check it on a one-GPU box
+    use_dist = world > 1 or os.environ.get("SM_BENCH_DIST") == "1"
+    out_fd = 1
+    if use_dist:
+        # RCCL prints its version banner on stdout when a communicator comes up: keep stdout for
+        # the one JSON line (written to the saved descriptor) and send everything else to stderr
+        sys.stdout.flush()
+        out_fd = os.dup(1)
+        os.dup2(2, 1)
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(s.getsockname()[1])
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
     torch.cuda.set_device(dev)
     sm = load_package_cached()
@@ -486,11 +501,11 @@ def main():
     # ---- headline: configs 2 + 3, weak scaling -------------------------------------------
     blocks_np = text_blocks(args.blocks, 0x5EED + rank)
     batch = Batch(blocks_np, dev)
-    sizes_all = torch.zeros(world * args.blocks, dtype=torch.int32, device=dev) if world > 1 else None
+    sizes_all = torch.zeros(world * args.blocks, dtype=torch.int32, device=dev) if use_dist else None
 
     def step():
         batch.compress(sm)
-        if world > 1:
+        if use_dist:
             dist.all_gather_into_tensor(sizes_all, batch.comp_len)
         batch.uncompress(sm)
 
@@ -589,7 +604,7 @@ def main():
         extras["config5_host_stream"] = config5_host_stream(sm, big)
         ok_all &= extras["config5_host_stream"]["ok"]
 
-    if world > 1:
+    if use_dist:
         t = torch.tensor([0 if ok_all else 1], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ok_all = int(t.item()) == 0
@@ -631,8 +646,9 @@ def main():
             "cpu_baseline": cpu,
         }
         line.update(extras)
-        print(json.dumps(line), flush=True)
-    if world > 1:
+        sys.stdout.flush()
+        os.write(out_fd, (json.dumps(line) + "\n").encode())
+    if use_dist:
         dist.destroy_process_group()
     if not ok_all:
         sys.exit(3)

@@ -91,3 +91,46 @@ def test_fragment_bounds_match_reference_loop():
         assert (lens > 0).all()
         assert len(offs) == (n + 65535) // 65536
     assert D.varint32(675282944) == bytes.fromhex("80 80 80 c2 02".replace(" ", ""))
+
+
+def _offsets_worker(rank, world, port, total, q):
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        load_package()
+        from importlib import import_module
+        D = import_module("snappy_jl_amd.dist")
+        nfrag = (total + 65535) // 65536
+        lo, hi = D.shard_range(nfrag, rank, world)
+        # stand-in fragment sizes, a function of the global fragment index
+        local = torch.tensor([1000 + (7919 * i) % 5000 for i in range(lo, hi)], dtype=torch.int32)
+        offs, tot = D.stream_offsets_device(local, total, rank, world)
+        q.put((rank, offs.tolist(), int(tot.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_stream_offsets_device_world(world):
+    """bench.py's config-5 index (the RCCL all-gather path, gloo here) equals the serial scan."""
+    total = 675282944 // 64 + 12345  # 162 fragments, ragged tail
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_offsets_worker, args=(r, world, port, total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    outs = {r: (o, t) for r, o, t in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nfrag = (total + 65535) // 65536
+    sizes = [1000 + (7919 * i) % 5000 for i in range(nfrag)]
+    hl = 4  # varint(10563041)
+    starts = list(hl + np.concatenate([[0], np.cumsum(sizes)[:-1]]))
+    got = [x for r in range(world) for x in outs[r][0]]
+    assert got == [int(x) for x in starts]
+    assert all(outs[r][1] == hl + sum(sizes) for r in range(world))
