@@ -80,7 +80,8 @@ void sm_ctx_destroy(sm_ctx* ctx);
 /* the HIP stream the ctx launches on (hipStream_t) */
 void* sm_ctx_stream(sm_ctx* ctx);
 /* diagnostic: how the ctx's last sm_uncompress decoded -- 0 in stream order (one wave),
- * 1 as parallel 64 KiB fragments (a large block-structured stream), -1 none yet */
+ * 1 as parallel 64 KiB fragments (a large block-structured stream), 2 in parallel by origin
+ * pointers (a large stream whose copies cross 64 KiB blocks), -1 none yet */
 int sm_ctx_last_path(sm_ctx* ctx);
 
 /* ---- single buffer, host memory (the reference's exported API) -------------------- */

@@ -64,7 +64,7 @@ struct HostBuf {  // pinned host staging (one D2H transfer per batch call)
 struct sm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
-  DevBuf in, out, out2, meta, idx, gat;
+  DevBuf in, out, out2, meta, idx, gat, org;  // org: origin pointers of the general parallel decode
   HostBuf stage;
   int last_path = -1;  // sm_ctx_last_path
   std::mutex mu;       // serialises the host-buffer entry points (they share the scratch above)
@@ -137,7 +137,7 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
   // true path: chunk entries y, output before them O, output of their tags
   struct PathChunk {
-    uint64_t y, O, out;
+    uint64_t y, O, out, ex;
   };
   std::vector<PathChunk> path;
   uint64_t y = ip0, O = 0;
@@ -150,7 +150,7 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
     } else {
       host_walk(comp, n, y, std::min<uint64_t>(base + kIdxChunk, (uint64_t)n - 1), &ex, &ot);
     }
-    path.push_back({y, O, ot});
+    path.push_back({y, O, ot, ex});
     O += ot;
     if (O > size || ex <= y) return 0;
     y = ex;
@@ -174,9 +174,48 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   std::vector<int32_t> st(nfrag);
   if (hipMemcpyAsync(st.data(), d_st, nfrag * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
-  for (int32_t v : st)
+  bool cross = false;
+  for (int32_t v : st) {
+    if (v == sm::kErrCross) cross = true;
+    else if (v != sm::kOk) return 0;  // an error: the in-order decode reports it exactly
+  }
+  if (!cross) return 1;
+  // Not block-structured (a copy reaches into an earlier block): origin pointers per output
+  // byte, resolved by pointer jumping (sm_decompress.hip, "any large stream").
+  if (n >= 0x80000000u || size >= 0x80000000u) return 0;  // 31-bit positions
+  const size_t npath = path.size();
+  std::vector<sm::OriginPath> op(npath);
+  for (size_t e = 0; e < npath; ++e)
+    op[e] = {(uint32_t)path[e].y, (uint32_t)path[e].ex, (uint32_t)path[e].O, (uint32_t)path[e].out};
+  const size_t p_off = 0, path_off = align_up((size_t)size * 4, 256), st2_off = align_up(path_off + npath * 16, 256);
+  const size_t pend_off = align_up(st2_off + npath * 4, 256);
+  if (ctx->org.ensure(pend_off + 16) != hipSuccess) return -1;
+  uint8_t* ob = (uint8_t*)ctx->org.p;
+  uint32_t* d_P = (uint32_t*)(ob + p_off);
+  sm::OriginPath* d_path = (sm::OriginPath*)(ob + path_off);
+  int32_t* d_st2 = (int32_t*)(ob + st2_off);
+  uint32_t* d_pend = (uint32_t*)(ob + pend_off);
+  if (hipMemcpyAsync(d_path, op.data(), npath * sizeof(sm::OriginPath), hipMemcpyHostToDevice, s) != hipSuccess)
+    return -1;
+  if (sm::launch_origin_fill(d_in, n, size, d_path, (uint32_t)npath, d_P, d_st2, s) != hipSuccess) return -1;
+  std::vector<int32_t> st2(npath);
+  if (hipMemcpyAsync(st2.data(), d_st2, npath * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  for (int32_t v : st2)
     if (v != sm::kOk) return 0;
-  return 1;
+  // round k moves every unresolved pointer >= 2^k chain steps: 32 rounds cover any size
+  bool done = false;
+  for (int round = 0; round < 32 && !done; ++round) {
+    uint32_t pend = 0;
+    if (hipMemsetAsync(d_pend, 0, 4, s) != hipSuccess) return -1;
+    if (sm::launch_origin_resolve(d_P, size, d_pend, s) != hipSuccess) return -1;
+    if (hipMemcpyAsync(&pend, d_pend, 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    done = pend == 0;
+  }
+  if (!done) return 0;
+  if (sm::launch_origin_gather(d_in, d_P, size, (uint8_t*)ctx->out.p, s) != hipSuccess) return -1;
+  return 2;
 }
 
 }  // namespace
@@ -388,6 +427,7 @@ void sm_ctx_destroy(sm_ctx* ctx) {
     ctx->meta.release();
     ctx->idx.release();
     ctx->gat.release();
+    ctx->org.release();
     ctx->stage.release();
     (void)hipStreamDestroy(ctx->stream);
   }
@@ -690,8 +730,8 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   if (size >= kParallelMinOutput && n - hdr >= 2 * sm::kIdxChunk) {
     const int r = parallel_uncompress(ctx, (const uint8_t*)compressed, (uint32_t)n, (uint32_t)hdr, size);
     if (r < 0) return SM_ERR_DEVICE;
-    if (r == 1) {
-      ctx->last_path = 1;
+    if (r >= 1) {
+      ctx->last_path = r;
       SM_CHECK(hipMemcpyAsync(uncompressed, ctx->out.p, size, hipMemcpyDeviceToHost, s));
       SM_CHECK(hipStreamSynchronize(s));
       *uncompressed_length = size;

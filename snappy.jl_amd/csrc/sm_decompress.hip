@@ -958,6 +958,135 @@ hipError_t launch_uncompressed_length(const uint8_t* in, const uint64_t* in_off,
   return hipGetLastError();
 }
 
+// ---- any large stream, decoded in parallel by origin pointers ---------
+// A stream whose copies reach into earlier 64 KiB blocks (not block-structured) cannot be cut
+// into independent fragments.  Its output is still a pure function of the tags: output byte x
+// is a literal byte in[i] or, inside a copy with offset d, the byte at x - d.  With the tag
+// path of k_stream_index (host-chained: path element e = the tags starting in [y_e, ex_e),
+// whose output starts at O_e):
+//  1. k_origin_fill, one wave per path element: walk the element's tags (walk_window over
+//     64-B-strided global words), apply the reference's checks (src/internal.jl:499,505,518),
+//     and write P[x] for every output byte: 0x80000000 | i for a literal byte in[i], x - d for
+//     a copy byte;
+//  2. k_origin_resolve rounds: P[x] = P[P[x]] while P[x] names a copy byte.  Every value stays
+//     an earlier byte of x's copy chain (in-place updates only move along it), and round k
+//     moves an unresolved pointer at least 2^k steps, so ceil(log2(size)) rounds finish;
+//  3. k_origin_gather: out[x] = in[P[x] & 0x7fffffff].
+// The result is the plain LZ77 meaning of the tags -- decompress_all_tags!'s output for a valid
+// stream (incremental_copy_slow!, internal.jl:477-481).  Any check that fails sends the caller
+// to the in-order decode, which returns the reference's exact status.
+
+__device__ inline uint64_t load8z(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
+  return (uint64_t)load_word(in, N, p) | ((uint64_t)load_word(in, N, p + 4) << 32);
+}
+
+__global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
+                                                    const OriginPath* path, uint32_t* __restrict__ P,
+                                                    int32_t* status) {
+  __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
+  const uint32_t lane = lane_id();
+  const OriginPath pe = path[blockIdx.x];
+  uint32_t ip = pe.y, op = pe.O;
+  int32_t st = kOk;
+  const uint32_t end = min(pe.ex, N - 1);  // a tag on the last byte is never parsed (internal.jl:416)
+  while (ip < end) {
+    const uint32_t rlim = min(256u, end - ip);  // tags that start before ex
+    uint32_t cpos, csz, sizes;
+    const uint32_t ntok = walk_window(load8z(in, N, ip + 4 * lane), rlim, jt, lane, cpos, csz, sizes);
+    if (ntok == 0) {  // a literal too long for a window walk (or a wrapped length): whole wave
+      const uint64_t hv = load8z(in, N, ip);
+      const uint32_t c = uniform((uint32_t)hv & 0xff);
+      const uint32_t entry = char_entry(c);
+      const uint32_t taglen = entry >> 11;
+      const uint32_t tr_raw = uniform((uint32_t)(hv >> 8));
+      const uint32_t trailer = taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * taglen)) - 1u));
+      const uint32_t litlen = (entry & 0xff) + trailer;  // u32 wrap, as the reference
+      const uint64_t lsrc = (uint64_t)ip + 1 + taglen;
+      if ((c & 3) || lsrc + litlen > N || (uint64_t)op + litlen > size) {  // :518 (a copy here: bad path)
+        st = kErrLiteral;
+        break;
+      }
+      for (uint32_t i = lane; i < litlen; i += kWave) P[op + i] = 0x80000000u | (uint32_t)(lsrc + i);
+      op += litlen;
+      ip = (uint32_t)(lsrc + litlen);
+      continue;
+    }
+    const bool mine = lane < ntok;
+    const uint32_t tpos = ip + (mine ? cpos : 0u);
+    const uint64_t hv = load8z(in, N, tpos);
+    const uint32_t c = (uint32_t)hv & 0xff;
+    const uint32_t entry = char_entry(c);
+    const uint32_t len = entry & 0xff;
+    const uint32_t taglen = entry >> 11;
+    const uint32_t tr_raw = (uint32_t)(hv >> 8);
+    const uint32_t trailer = taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * taglen)) - 1u));
+    const bool iscopy = (c & 3) != 0;
+    const uint32_t offset = (entry & 0x700) + trailer;
+    const uint32_t litlen = len + trailer;
+    const uint32_t olen = mine ? (iscopy ? len : litlen) : 0u;
+    const uint32_t incl = scan_dpp(olen);
+    const uint32_t opt = op + incl - olen;
+    const uint32_t lsrc = tpos + 1 + taglen;
+    const bool bad = mine && (iscopy ? (offset == 0 || offset > opt || (uint64_t)opt + len > size)     // :499, :505
+                                     : ((uint64_t)lsrc + litlen > N || (uint64_t)opt + litlen > size));  // :518
+    if (ballot(bad)) {
+      st = kErrInvalid;
+      break;
+    }
+    // every output byte of the window's tags: tag t's bytes by the whole wave
+    for (uint32_t t = 0; t < ntok; ++t) {
+      const uint32_t o = readlane(opt, t), L = readlane(olen, t);
+      const uint32_t v0 = readlane(iscopy ? 0u - offset : (0x80000000u | lsrc) - o, t);  // P[o+i] = o + i + v0
+      for (uint32_t i = lane; i < L; i += kWave) P[o + i] = o + i + v0;
+    }
+    op += readlane(incl, ntok - 1);
+    ip += readlane(cpos + csz, ntok - 1);
+  }
+  if (st == kOk && ip != pe.ex && !(ip >= end && pe.ex >= end)) st = kErrInvalid;  // tags tile the path
+  if (st == kOk && op != pe.O + pe.out) st = kErrInvalid;
+  if (lane == 0) status[blockIdx.x] = st;
+}
+
+__global__ __launch_bounds__(256) void k_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending) {
+  uint32_t left = 0;
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < size; x += gridDim.x * blockDim.x) {
+    const uint32_t v = P[x];
+    if (!(v >> 31)) {
+      const uint32_t w = P[v];  // v < x: an earlier byte of the chain
+      P[x] = w;
+      left += !(w >> 31);
+    }
+  }
+  if (__builtin_amdgcn_ballot_w64(left != 0) && lane_id() == 0) atomicAdd(pending, 1u);
+}
+
+__global__ __launch_bounds__(256) void k_origin_gather(const uint8_t* __restrict__ in, const uint32_t* __restrict__ P,
+                                                       uint32_t size, uint8_t* __restrict__ out) {
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < size; x += gridDim.x * blockDim.x)
+    out[x] = in[P[x] & 0x7fffffffu];
+}
+
+hipError_t launch_origin_fill(const uint8_t* in, uint32_t N, uint32_t size, const OriginPath* path, uint32_t npath,
+                              uint32_t* P, int32_t* status, hipStream_t s) {
+  if (npath == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_origin_fill, dim3(npath), dim3(64), 0, s, in, N, size, path, P, status);
+  return hipGetLastError();
+}
+
+static uint32_t origin_grid(uint32_t size) { return min(8192u, max(1u, (size + 1023) / 1024)); }
+
+hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, hipStream_t s) {
+  if (size == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_origin_resolve, dim3(origin_grid(size)), dim3(256), 0, s, P, size, pending);
+  return hipGetLastError();
+}
+
+hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s) {
+  if (size == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_origin_gather, dim3(origin_grid(size)), dim3(256), 0, s, in, P, size, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec_exit,
                                uint32_t* rec_out, hipStream_t s) {
   if (nchunks == 0) return hipSuccess;

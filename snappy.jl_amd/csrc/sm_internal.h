@@ -58,6 +58,16 @@ hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint
                                uint32_t* rec_out, hipStream_t s);
 hipError_t launch_decompress_frags(const uint8_t* in, uint32_t N, uint32_t size, uint8_t* out,
                                    const StreamFrag* frags, uint32_t nfrag, int32_t* status, hipStream_t s);
+// Any large stream (copies may reach into earlier blocks): origin pointers per output byte,
+// resolved by pointer jumping (sm_decompress.hip).  Path element = the tags starting in [y, ex),
+// whose out bytes of output start at O.
+struct OriginPath {
+  uint32_t y, ex, O, out;
+};
+hipError_t launch_origin_fill(const uint8_t* in, uint32_t N, uint32_t size, const OriginPath* path, uint32_t npath,
+                              uint32_t* P, int32_t* status, hipStream_t s);
+hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, hipStream_t s);
+hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)
 hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
                          const uint64_t* dst_off, uint8_t* dst, uint32_t nblk, hipStream_t s);

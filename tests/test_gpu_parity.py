@@ -352,16 +352,18 @@ def test_uncompress_large_stream_parallel(sm, oracle, libsnappy, gpu_available):
 
 def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
     """Valid streams that are not block-structured (copies into earlier 64 KiB blocks, a
-    literal across a fragment start) and corrupted large streams take the in-order decode,
-    with the oracle's output and status."""
+    literal across a fragment start) decode in parallel by origin pointers (path 2) with the
+    oracle's output; corrupted large streams take the in-order decode, with the oracle's
+    status."""
     from streams import build, random_ops
     rng = np.random.default_rng(31)
     s1, e1 = build(random_ops(rng, 400_000))                        # offsets up to 65535
     s2, e2 = build([("lit", rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes())] +
                    [("copy", 1000, 64)] * 5000)                      # literal across 65536
     for s, e in ((s1, e1), (s2, e2)):
+        assert oracle.uncompress(s) == e
         assert sm.uncompress(s) == e
-        assert sm.last_uncompress_path() == 0
+        assert sm.last_uncompress_path() == 2
     good = oracle.compress(_big_corpus(600_000))
     for i in range(40):
         bad = bytearray(good)
@@ -464,3 +466,41 @@ def sys_path_root():
     import sys
     if ROOT not in sys.path:
         sys.path.insert(0, ROOT)
+
+
+def test_uncompress_origin_path_cases(sm, oracle, gpu_available):
+    """The origin-pointer parallel decode (path 2) on streams built to stress it: deep copy
+    chains (offset 1 runs over 300 KB: 18+ pointer-jumping rounds), copy-4 offsets past 64 KiB,
+    overlapping copies of every offset 1..20, long literals between copies, and a stream whose
+    every copy reaches exactly to the start of the output.  Output equals the oracle's."""
+    from streams import build, random_ops
+    rng = np.random.default_rng(77)
+    cases = []
+    # a 1-byte seed, then offset-1 copies: one chain through the whole output
+    cases.append(build([("lit", b"x")] + [("copy", 1, 64)] * 5000))
+    # copy-4: offsets beyond 64 KiB into a long random prefix
+    pre = rng.integers(0, 256, 200_000, dtype=np.uint8).tobytes()
+    ops = [("lit", pre)]
+    for _ in range(6000):
+        ops.append(("copy", int(rng.integers(65_536, 200_000)), int(rng.integers(4, 65))))
+    cases.append(build(ops))
+    # overlapping copies of small offsets, interleaved with literals (some long)
+    ops = [("lit", rng.integers(0, 256, 64, dtype=np.uint8).tobytes())]
+    for i in range(20_000):
+        if i % 97 == 0:
+            ops.append(("lit", rng.integers(0, 256, int(rng.integers(201, 2000)), dtype=np.uint8).tobytes()))
+        ops.append(("copy", 1 + i % 20, int(rng.integers(1, 65))))
+    cases.append(build(ops))
+    # every copy reaches back to byte 0 (offset = produced)
+    ops, size = [("lit", rng.integers(0, 256, 5000, dtype=np.uint8).tobytes())], 5000
+    for _ in range(8000):
+        ln = int(rng.integers(4, 65))
+        ops.append(("copy", size, ln))
+        size += ln
+    cases.append(build(ops))
+    cases.append(build(random_ops(rng, 1_500_000, max_off=65535, near=60_000)))
+    for s, e in cases:
+        assert oracle.uncompress(s) == e
+        assert sm.uncompress(s) == e
+        assert sm.last_uncompress_path() == 2
+        assert sm.validate(s) == 0
