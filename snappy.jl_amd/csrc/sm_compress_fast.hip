@@ -186,13 +186,25 @@ struct Cfg {
   static constexpr uint32_t kRingBytes = 2 * kRoundPos * sizeof(Cand);
 };
 
-// Inserter: positions [r0, r0 + kRoundPos) in order; ring[i] receives the candidates of
-// position r0 + i (the old table entry).  kG groups of 64 positions per step so the LDS round
-// trips overlap.  r0 is a multiple of 64: the words come from aligned dwords (immediate
-// offsets), and reads past n stay inside the LDS allocation (the table follows the block).
+// Hashes of one group of 64 positions [base, base + 64) (base a multiple of 64) into hr[lane]:
+// the words come from aligned dwords (one ds_read2), so reads past n stay inside the LDS
+// allocation (the table follows the block).  Positions without 4 bytes hash garbage: the
+// inserter still inserts them (no exec masks), which is harmless -- they are the block's last
+// positions, so no valid position is ever handed one of them as a candidate (later positions
+// are all invalid too, and within one exchange the lower lanes go first).
+template <typename Cand>
+__device__ inline void hash_group(const uint8_t* data, Cand* hr, uint32_t base, uint32_t lane) {
+  const uint32_t* dw = reinterpret_cast<const uint32_t*>(data + base) + (lane >> 2);
+  hr[lane] = (Cand)fast_hash<kTabBits>(__builtin_amdgcn_alignbyte(dw[1], dw[0], lane & 3u));
+}
+
+// Inserter: positions [r0, r0 + kRoundPos) in order.  ring[i] holds the hash of position r0 + i
+// (written by the parse waves, hash_group) and receives its candidates: the old table entry.
+// The inserter's own work is three LDS instructions per 64 positions (read the hashes, exchange,
+// write the candidates), kG groups per step so the round trips overlap; the hashing is the
+// parse waves' (it was 80% of this single wave's issue slots, the floor under every round).
 template <int D>
-__device__ inline void insert_round(const uint8_t* data, uint32_t* T, typename Cfg<D>::Cand* ring, uint32_t r0,
-                                    uint32_t n, uint32_t lane) {
+__device__ inline void insert_round(uint32_t* T, typename Cfg<D>::Cand* ring, uint32_t r0, uint32_t n, uint32_t lane) {
 #ifndef SM_FAST_KG
 #define SM_FAST_KG 6
 #endif
@@ -200,52 +212,37 @@ __device__ inline void insert_round(const uint8_t* data, uint32_t* T, typename C
   constexpr uint32_t kRP = Cfg<D>::kRoundPos;
   static_assert((kRP / 64) % kG == 0, "insert step");
   if (r0 >= n) return;
+  // only groups whose chunk exists have hashes in the ring (a short last round stops at n)
   const uint32_t ngroups = min((n - r0 + 63) >> 6, kRP / 64);
-  const bool full = r0 + kRP + 3 <= n;  // every position of the round has its 4 bytes
-  const uint32_t sh = lane & 3u;
-  // software pipeline: the next step's words are read right behind this step's exchanges, so
-  // the two LDS round trips of a step overlap
-  uint32_t h[kG];
-  bool ok[kG];
-  auto hash_step = [&](uint32_t g0, uint32_t* hh, bool* oo) {
-    const uint32_t base = r0 + 64 * g0;
-    const uint32_t* dw = reinterpret_cast<const uint32_t*>(data + base) + (lane >> 2);
+  auto step = [&](uint32_t g0, uint32_t (&h)[kG], bool guarded) {
+    const uint32_t pos1 = r0 + 64 * g0 + lane + 1;
+    uint32_t old[kG], hn[kG];
+#pragma unroll
+    for (int i = 0; i < kG; ++i)
+      if (!guarded || g0 + i < ngroups)
+        old[i] = __hip_atomic_exchange(&T[h[i]], pos1 + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // the next step's hashes, behind this step's exchanges
+#pragma unroll
+    for (int i = 0; i < kG; ++i)
+      if (g0 + kG + i < ngroups) hn[i] = ring[64 * (g0 + kG + i) + lane];
 #pragma unroll
     for (int i = 0; i < kG; ++i) {
-      hh[i] = fast_hash<kTabBits>(__builtin_amdgcn_alignbyte(dw[16 * i + 1], dw[16 * i], sh));
-      oo[i] = base + 64 * i + lane + 4 <= n;
-    }
-  };
-  hash_step(0, h, ok);
-  for (uint32_t g0 = 0; g0 < ngroups; g0 += kG) {
-    const uint32_t base = r0 + 64 * g0;
-    uint32_t old[kG], hn[kG];
-    bool okn[kG];
-    if (full) {  // a uniform branch: every lane exchanges, no per-exchange exec masks
-#pragma unroll
-      for (int i = 0; i < kG; ++i)
-        old[i] = __hip_atomic_exchange(&T[h[i]], base + 64 * i + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    } else {
-#pragma unroll
-      for (int i = 0; i < kG; ++i) {
-        old[i] = 0;
-        if (ok[i])
-          old[i] = __hip_atomic_exchange(&T[h[i]], base + 64 * i + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (!guarded || g0 + i < ngroups) {
+        // the old latest becomes the second-latest (the new entry's high half)
+        if (D > 1) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];  // (dense only)
+        ring[64 * (g0 + i) + lane] = (typename Cfg<D>::Cand)old[i];
       }
     }
-    if (g0 + kG < ngroups) hash_step(g0 + kG, hn, okn);
 #pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      // the old latest becomes the second-latest (the new entry's high half)
-      if (D > 1 && (full || ok[i])) reinterpret_cast<uint16_t*>(&T[h[i]])[1] = (uint16_t)old[i];  // (dense only)
-      ring[64 * (g0 + i) + lane] = (typename Cfg<D>::Cand)old[i];
-    }
+    for (int i = 0; i < kG; ++i) h[i] = hn[i];
+  };
+  uint32_t h[kG];
 #pragma unroll
-    for (int i = 0; i < kG; ++i) {
-      h[i] = hn[i];
-      ok[i] = okn[i];
-    }
-  }
+  for (int i = 0; i < kG; ++i)
+    if ((uint32_t)i < ngroups) h[i] = ring[64 * i + lane];
+  uint32_t g0 = 0;
+  for (; g0 + kG <= ngroups; g0 += kG) step(g0, h, false);  // full steps: no exec or scalar guards
+  if (g0 < ngroups) step(g0, h, true);
 }
 
 // A parsed chunk, held in registers from its parse to its emission after the round barrier.
@@ -675,9 +672,13 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
 
   const uint32_t nchunks = (n + kChunk - 1) / kChunk;
   const uint32_t rounds = (nchunks + kSlots - 1) / kSlots;
+  // hashes of rounds 0 and 1 (the ring's two halves) by every wave; later rounds' hashes are
+  // written by the parse waves into the slots whose candidates they have just read
+  for (uint32_t g = wave; g < 2 * kRP / 64 && 64 * g < n; g += kWavesPerBlock) hash_group(data, ring + 64 * g, 64 * g, lane);
+  __syncthreads();
   // the inserter shares a SIMD with three parse waves and gates every round: issue it first
   if (inserter && SM_FAST_PRIO) __builtin_amdgcn_s_setprio(SM_FAST_PRIO);
-  if (inserter) insert_round<kDepth>(data, T, ring, 0, n, lane);
+  if (inserter) insert_round<kDepth>(T, ring, 0, n, lane);
   __syncthreads();
 
   STAMP_DECL
@@ -688,7 +689,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     uint32_t* cinfo = csize + (r & 1) * 32;
     ChunkTok tk[C::kCPW];
     if (inserter) {
-      insert_round<kDepth>(data, T, ring + ((r + 1) & 1) * kRP, (r + 1) * kRP, n, lane);
+      insert_round<kDepth>(T, ring + ((r + 1) & 1) * kRP, (r + 1) * kRP, n, lane);
       STAMP(8)
       STAMP_COUNT(10, 1)
     } else {
@@ -700,12 +701,26 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
         const uint32_t c0 = k * kChunk;
         if (SM_FAST_PPRIO && u == 0) __builtin_amdgcn_s_setprio(1);
         if (SM_FAST_PPRIO && u == 1) __builtin_amdgcn_s_setprio(0);
-        if (k < nchunks && !(SM_ABLATE & 4)) {
+        if (k < nchunks && (SM_ABLATE & 4)) {  // diagnostic: hashes only (the inserter needs them)
+          Cand* cr = ring + (r & 1) * kRP + slot * kChunk;
+          if (k + 2 * kSlots < nchunks) {
+#pragma unroll
+            for (int j = 0; j < kP; ++j) hash_group(data, cr + 64 * j, c0 + 2 * kRP + 64 * j, lane);
+          }
+          tk[u].c0 = tk[u].ce = c0;
+          if (lane == 0) cinfo[slot] = 0;
+        } else if (k < nchunks) {
           STAMP_COUNT(11, 1)
-          const Cand* cr = ring + (r & 1) * kRP + slot * kChunk;
+          Cand* cr = ring + (r & 1) * kRP + slot * kChunk;
           uint32_t cv[kP];
 #pragma unroll
           for (int j = 0; j < kP; ++j) cv[j] = cr[64 * j + lane];
+          // the same slot of round r + 2 (this ring half's next use): its hashes, in place
+          // (the reads above are this lane's, and a wave's LDS instructions run in order)
+          if (k + 2 * kSlots < nchunks) {
+#pragma unroll
+            for (int j = 0; j < kP; ++j) hash_group(data, cr + 64 * j, c0 + 2 * kRP + 64 * j, lane);
+          }
           const uint32_t info = parse_chunk<kDepth>(data, cv, jt, tsw, c0, min(c0 + kChunk, n), n, lane, tk[u]);
           if (lane == 0) cinfo[slot] = info;
         } else {
