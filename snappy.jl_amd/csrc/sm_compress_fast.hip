@@ -37,7 +37,6 @@
 
 namespace sm {
 
-constexpr uint32_t kScreenTodo = 0xfffffffeu;  // out_len mark of k_literal_screen: the parse compresses this block
 
 #if SM_STAMP
 __device__ unsigned long long g_stamp_c[12];
@@ -58,6 +57,12 @@ constexpr int kP = kChunk / 64;                // positions per lane
 // ratio 0.578 instead of 0.598 on the bench text but runs 7% slower (more copies to parse).
 constexpr uint32_t kTabBits = 13;
 constexpr uint32_t kTabBytes = 4u << kTabBits;
+// SM_FAST_T16: depth 1 uses the same 32 KiB as 16 K u16 buckets (14-bit hash), exchanged with
+// ds_mskor_rtn_b32 (a masked exchange of one half-dword; inline asm: no builtin exists)
+#ifndef SM_FAST_T16
+#define SM_FAST_T16 0
+#endif
+constexpr bool kTab16 = SM_FAST_T16;
 constexpr uint32_t kWavesPerBlock = 16;
 constexpr uint32_t kPW = kWavesPerBlock - 1;  // parse waves; wave kPW is the inserter
 constexpr uint32_t kThreads = 64 * kWavesPerBlock;
@@ -88,6 +93,7 @@ constexpr bool kShortCopies = SM_FAST_LCAP != 0 && SM_FAST_LCAP <= 64;  // one p
 #define SM_FAST_XCOMPACT 1
 #endif
 constexpr bool kXCompact = SM_FAST_XCOMPACT && kChunk == 256;  // extension jobs compacted (below)
+constexpr uint32_t kVW = 8;  // bytes the verification compares (16: equal time, round 2)
 
 // literal tag bytes for a run of len bytes (0 = no run): emit_literal! (internal.jl:271-284)
 __device__ inline uint32_t lit_tag_bytes(uint32_t len) { return len == 0 ? 0u : (len <= 60 ? 1u : (len <= 256 ? 2u : 3u)); }
@@ -194,8 +200,9 @@ struct Cfg {
 // are all invalid too, and within one exchange the lower lanes go first).
 template <typename Cand>
 __device__ inline void hash_group(const uint8_t* data, Cand* hr, uint32_t base, uint32_t lane) {
+  constexpr uint32_t kBits = (kTab16 && sizeof(Cand) == 2) ? kTabBits + 1 : kTabBits;
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(data + base) + (lane >> 2);
-  hr[lane] = (Cand)fast_hash<kTabBits>(__builtin_amdgcn_alignbyte(dw[1], dw[0], lane & 3u));
+  hr[lane] = (Cand)fast_hash<kBits>(__builtin_amdgcn_alignbyte(dw[1], dw[0], lane & 3u));
 }
 
 // Inserter: positions [r0, r0 + kRoundPos) in order.  ring[i] holds the hash of position r0 + i
@@ -217,10 +224,41 @@ __device__ inline void insert_round(uint32_t* T, typename Cfg<D>::Cand* ring, ui
   auto step = [&](uint32_t g0, uint32_t (&h)[kG], bool guarded) {
     const uint32_t pos1 = r0 + 64 * g0 + lane + 1;
     uint32_t old[kG], hn[kG];
+    if (kTab16 && D == 1) {
+      // bucket h is half (h & 1) of dword h >> 1: D = (D & ~mask) | value, the old dword back.
+      // The six exchanges and their wait are ONE asm statement (early-clobber results), so the
+      // compiler cannot touch a result register before the data has returned; a group past the
+      // round's end exchanges with mask 0 (memory unchanged).
+      uint32_t la[kG], mk[kG], vv[kG];
 #pragma unroll
-    for (int i = 0; i < kG; ++i)
-      if (!guarded || g0 + i < ngroups)
-        old[i] = __hip_atomic_exchange(&T[h[i]], pos1 + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int i = 0; i < kG; ++i) {
+        const bool v = !guarded || g0 + i < ngroups;
+        const uint32_t hh = v ? h[i] : 0u, sh = (hh & 1u) << 4;
+        la[i] = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)(&T[hh >> 1]));
+        mk[i] = v ? 0xffffu << sh : 0u;
+        vv[i] = v ? (pos1 + 64 * i) << sh : 0u;
+      }
+      static_assert(kG == 6, "the asm below issues kG exchanges");
+      asm volatile(
+          "ds_mskor_rtn_b32 %0, %6, %12, %18\n"
+          "ds_mskor_rtn_b32 %1, %7, %13, %19\n"
+          "ds_mskor_rtn_b32 %2, %8, %14, %20\n"
+          "ds_mskor_rtn_b32 %3, %9, %15, %21\n"
+          "ds_mskor_rtn_b32 %4, %10, %16, %22\n"
+          "ds_mskor_rtn_b32 %5, %11, %17, %23\n"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(old[0]), "=&v"(old[1]), "=&v"(old[2]), "=&v"(old[3]), "=&v"(old[4]), "=&v"(old[5])
+          : "v"(la[0]), "v"(la[1]), "v"(la[2]), "v"(la[3]), "v"(la[4]), "v"(la[5]), "v"(mk[0]), "v"(mk[1]), "v"(mk[2]),
+            "v"(mk[3]), "v"(mk[4]), "v"(mk[5]), "v"(vv[0]), "v"(vv[1]), "v"(vv[2]), "v"(vv[3]), "v"(vv[4]), "v"(vv[5])
+          : "memory");
+#pragma unroll
+      for (int i = 0; i < kG; ++i) old[i] = (old[i] >> ((h[i] & 1u) << 4)) & 0xffffu;
+    } else {
+#pragma unroll
+      for (int i = 0; i < kG; ++i)
+        if (!guarded || g0 + i < ngroups)
+          old[i] = __hip_atomic_exchange(&T[h[i]], pos1 + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     // the next step's hashes, behind this step's exchanges
 #pragma unroll
     for (int i = 0; i < kG; ++i)
@@ -329,7 +367,7 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const uint32_t (&cvi
 #pragma unroll
     for (int j = 0; j < kP; ++j) {
       const uint32_t q = c0 + 64 * j + lane;
-      const bool need = !(SM_ABLATE & 8) && Ls[j] >= 8 && Ls[j] < ext_lim(q);  // then Ls[j] == 8
+      const bool need = !(SM_ABLATE & 8) && Ls[j] >= kVW && Ls[j] < ext_lim(q);  // then Ls[j] == kVW
       JM[j] = ballot(need);
       if (need)
         jl[nj + __builtin_amdgcn_mbcnt_hi((uint32_t)(JM[j] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)JM[j], 0u))] =
@@ -343,7 +381,7 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const uint32_t (&cvi
         const uint32_t d = jl[act ? r0 + lane : 0];
         const uint32_t pos = d & 0xffu, q = c0 + pos;
         const uint32_t lim = ext_lim(q);
-        uint32_t L = 8;
+        uint32_t L = kVW;
         bool more = act;
         while (ballot(more)) {
           if (more) ext_step(q, d >> 8, lim, L, more);
@@ -362,7 +400,7 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const uint32_t (&cvi
       const uint32_t q = c0 + 64 * j + lane;
       uint32_t L = Ls[j];
       const uint32_t lim = ext_lim(q);
-      bool more = !(SM_ABLATE & 8) && L >= 8 && L < lim;
+      bool more = !(SM_ABLATE & 8) && L >= kVW && L < lim;
       while (ballot(more)) {
         if (more) ext_step(q, offs[j], lim, L, more);
       }
@@ -462,12 +500,12 @@ __device__ inline uint32_t parse_chunk(const uint8_t* data, const uint32_t (&cvi
     const uint64_t tm = ballot(istok);
     nmatch = (uint32_t)__builtin_popcountll(tm);
     const uint32_t sh = (uint32_t)(tm & 1u) ^ 1u;  // tokens start at lane 1 if 0 is no match
+    if (nmatch) last_end = readlane(c + Lc, nmatch - 1 + sh);
     // token: position | length << 16; offset
     const uint32_t tav = __shfl(c | (Lc << 16), lane + sh, 64), tbv = __shfl(vc >> 9, lane + sh, 64);
     if (nmatch) {
       t.ta = tav;
       t.tb = tbv;
-      last_end = readlane(c + Lc, nmatch - 1 + sh);
     }
     // copy-start bitmask (position p of the chunk) for the literal scatter
     if (lane < kP) tsw[lane] = 0;
@@ -934,7 +972,8 @@ hipError_t launch_compress_fast(const CompressArgs& a0, int mode, hipStream_t s)
   hipLaunchKernelGGL(k_literal_screen, dim3(a.nblk), dim3(kScrThreads), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return mode == 2 ? launch_depth<2>(a, s) : launch_depth<1>(a, s);
+  if (mode == 2) return launch_depth<2>(a, s);
+  return a.prev ? launch_compress_lanes(a, kLanesSub, s) : launch_depth<1>(a, s);
 }
 
 }  // namespace sm

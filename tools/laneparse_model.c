@@ -21,7 +21,7 @@ static uint32_t copy_bytes(uint32_t off, uint32_t len) { return (len < 12 && off
 static uint32_t hsh(uint32_t w, int bits) { return ((((w ^ (w >> 12)) & 0xffffff) * 0x1e35a7u) >> 10) & ((1u << bits) - 1); }
 
 static int LCAP = 64;
-static uint32_t ISTR = 1, PSTR = 1, OFFMAX = 65535;
+static uint32_t ISTR = 1, PSTR = 1, OFFMAX = 65535, NOMERGE = 0;
 
 static uint64_t model(const uint8_t* d, uint32_t n, int mode, uint32_t C, uint32_t K, int tb) {
   const uint32_t tab = 1u << tb;
@@ -46,6 +46,7 @@ static uint64_t model(const uint8_t* d, uint32_t n, int mode, uint32_t C, uint32
         }
       }
       uint32_t p = c0;
+      if (NOMERGE) { out += lit_bytes(c0 - ls); ls = c0; }
       while (p < ce) {
         uint32_t best = 0, bc = 0;
         if (p + 4 <= ce && p % PSTR == 0) {
@@ -92,12 +93,13 @@ int main(int argc, char** argv) {
   nb = fread(buf, 65536, nb, f);
   fclose(f);
   if (getenv("LCAP")) LCAP = atoi(getenv("LCAP"));
+  if (getenv("NOMERGE")) NOMERGE = 1;
   if (getenv("OFFMAX")) OFFMAX = atoi(getenv("OFFMAX"));
   if (getenv("ISTR")) ISTR = atoi(getenv("ISTR"));
   if (getenv("PSTR")) PSTR = atoi(getenv("PSTR"));
   int only0 = getenv("ONLY0") != 0;
   struct { int mode; uint32_t C, K; int tb; } cfg[] = {
-      {0, 256, 1, 13}, {0, 128, 1, 13}, {0, 64, 1, 13}, {0, 256, 1, 14}, {0, 1 << 16, 1, 13}, {0, 1 << 16, 1, 14},
+      {0, 256, 1, 13}, {0, 128, 1, 13}, {0, 64, 1, 13}, {0, 256, 1, 14}, {0, 128, 1, 14}, {0, 1 << 16, 1, 13}, {0, 1 << 16, 1, 14},
       {1, 256, 64, 13}, {1, 256, 16, 13}, {1, 128, 64, 13}, {1, 128, 32, 13}, {1, 128, 16, 13}, {1, 64, 64, 13},
       {1, 64, 32, 13}, {1, 64, 16, 13}, {1, 32, 64, 13}, {1, 64, 64, 14}, {1, 128, 32, 14},
       {2, 128, 32, 13}, {2, 64, 64, 13}, {2, 256, 64, 13},
