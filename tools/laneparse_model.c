@@ -99,7 +99,7 @@ int main(int argc, char** argv) {
   if (getenv("PSTR")) PSTR = atoi(getenv("PSTR"));
   int only0 = getenv("ONLY0") != 0;
   struct { int mode; uint32_t C, K; int tb; } cfg[] = {
-      {0, 256, 1, 13}, {0, 128, 1, 13}, {0, 64, 1, 13}, {0, 256, 1, 14}, {0, 128, 1, 14}, {0, 1 << 16, 1, 13}, {0, 1 << 16, 1, 14},
+      {0, 256, 1, 13}, {0, 128, 1, 13}, {0, 64, 1, 13}, {0, 256, 1, 14}, {0, 128, 1, 14}, {0, 64, 1, 14}, {0, 1 << 16, 1, 13}, {0, 1 << 16, 1, 14},
       {1, 256, 64, 13}, {1, 256, 16, 13}, {1, 128, 64, 13}, {1, 128, 32, 13}, {1, 128, 16, 13}, {1, 64, 64, 13},
       {1, 64, 32, 13}, {1, 64, 16, 13}, {1, 32, 64, 13}, {1, 64, 64, 14}, {1, 128, 32, 14},
       {2, 128, 32, 13}, {2, 64, 64, 13}, {2, 256, 64, 13},
