@@ -65,7 +65,6 @@ struct sm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   DevBuf in, out, out2, meta, idx, gat, org;  // org: origin pointers of the general parallel decode
-  DevBuf pv;  // SM_MODE_FAST: per-position candidates of a sub-batch (k_prev_insert -> k_compress_lanes)
   HostBuf stage;
   int last_path = -1;  // sm_ctx_last_path
   std::mutex mu;       // serialises the host-buffer entry points (they share the scratch above)
@@ -227,17 +226,6 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   } while (0)
 
 namespace {
-// SM_MODE_FAST compresses through k_prev_insert + k_compress_lanes, which exchange the
-// per-position candidates through the ctx's scratch (sub-batches of sm::kLanesSub blocks)
-hipError_t launch_compress_ctx(sm_ctx* ctx, sm::CompressArgs a, int mode, hipStream_t s) {
-  if (mode == SM_MODE_FAST && a.nblk) {
-    hipError_t e = ctx->pv.ensure(sm::lanes_scratch_bytes(a.nblk));
-    if (e != hipSuccess) return e;
-    a.prev = (uint16_t*)ctx->pv.p;
-  }
-  return sm::launch_compress(a, mode, s);
-}
-
 // Shard [b0, b1) of a host batch, rebased so the single-context call copies only the shard's
 // bytes: offsets relative to the shard's lowest input / output offset.
 struct Shard {
@@ -440,7 +428,6 @@ void sm_ctx_destroy(sm_ctx* ctx) {
     ctx->idx.release();
     ctx->gat.release();
     ctx->org.release();
-    ctx->pv.release();
     ctx->stage.release();
     (void)hipStreamDestroy(ctx->stream);
   }
@@ -457,7 +444,7 @@ sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint6
   if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return SM_ERR_ARGUMENT;
   DeviceGuard g(ctx->device);
   sm::CompressArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nblk, 0, 1};
-  SM_CHECK(launch_compress_ctx(ctx, a, mode, (hipStream_t)stream));
+  SM_CHECK(sm::launch_compress(a, mode, (hipStream_t)stream));
   return SM_OK;
 }
 
@@ -471,7 +458,7 @@ sm_status sm_compress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const u
   if (!d_in || !d_in_off || !d_in_len || !d_out || !d_out_off || !d_out_len) return SM_ERR_ARGUMENT;
   DeviceGuard g(ctx->device);
   sm::CompressArgs a{d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_len, nblk, sm::hashtable_size(total_len), 0};
-  SM_CHECK(launch_compress_ctx(ctx, a, mode, (hipStream_t)stream));
+  SM_CHECK(sm::launch_compress(a, mode, (hipStream_t)stream));
   return SM_OK;
 }
 
@@ -520,7 +507,7 @@ sm_status sm_compress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_o
   SM_CHECK(hipMemcpyAsync(d_in_len, in_len, 4 * (size_t)nblk, hipMemcpyHostToDevice, s));
   sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
                      nblk, 0, 1};
-  SM_CHECK(launch_compress_ctx(ctx, a, mode, s));
+  SM_CHECK(sm::launch_compress(a, mode, s));
   SM_CHECK(hipMemcpyAsync(out_len, d_out_len, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
   SM_CHECK(hipStreamSynchronize(s));
   // copy back only each block's bytes
@@ -692,7 +679,7 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   SM_CHECK(hipMemcpyAsync(d_in_len, in_len.data(), 4 * (size_t)nfrag, hipMemcpyHostToDevice, s));
   sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
                      nfrag, sm::hashtable_size(n), 0};
-  SM_CHECK(launch_compress_ctx(ctx, a, mode, s));
+  SM_CHECK(sm::launch_compress(a, mode, s));
   SM_CHECK(hipMemcpyAsync(out_len.data(), d_out_len, 4 * (size_t)nfrag, hipMemcpyDeviceToHost, s));
   SM_CHECK(hipStreamSynchronize(s));
   size_t total = 0;

@@ -37,6 +37,7 @@
 
 namespace sm {
 
+constexpr uint32_t kScreenTodo = 0xfffffffeu;  // out_len mark of k_literal_screen: the parse compresses this block
 
 #if SM_STAMP
 __device__ unsigned long long g_stamp_c[12];
@@ -972,8 +973,7 @@ hipError_t launch_compress_fast(const CompressArgs& a0, int mode, hipStream_t s)
   hipLaunchKernelGGL(k_literal_screen, dim3(a.nblk), dim3(kScrThreads), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if (mode == 2) return launch_depth<2>(a, s);
-  return a.prev ? launch_compress_lanes(a, kLanesSub, s) : launch_depth<1>(a, s);
+  return mode == 2 ? launch_depth<2>(a, s) : launch_depth<1>(a, s);
 }
 
 }  // namespace sm

@@ -19,14 +19,7 @@ struct CompressArgs {
   uint32_t table_size;  // 0: per block from its length (internal.jl:107-113); else fixed (Q2)
   int header;           // 1: prefix each block with varint(len) (independent snappy stream)
   int screened;         // set by launch_compress_fast: out_len holds k_literal_screen's verdicts
-  uint16_t* prev;       // SM_MODE_FAST scratch: min(nblk, kLanesSub) x 65536 u16 + 16 B (sm_compress_lanes.hip)
 };
-
-constexpr uint32_t kScreenTodo = 0xfffffffeu;  // out_len mark of k_literal_screen: the parse compresses this block
-constexpr uint32_t kLanesSub = 2048;           // blocks per k_prev_insert / k_compress_lanes sub-batch
-inline size_t lanes_scratch_bytes(uint32_t nblk) {
-  return (size_t)(nblk < kLanesSub ? nblk : kLanesSub) * 65536 * 2 + 16;
-}
 
 struct DecompressArgs {
   const uint8_t* in;
@@ -44,7 +37,6 @@ struct DecompressArgs {
 // mode 0 = reference (byte-identical to Snappy.jl), 1 = fast (wave-parallel parse), 2 = fast, denser
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s);
 hipError_t launch_compress_fast(const CompressArgs& a, int mode, hipStream_t s);
-hipError_t launch_compress_lanes(const CompressArgs& a, uint32_t sub, hipStream_t s);
 hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 
 // One large stream decoded in parallel (sm_uncompress): an index pass over 4 KiB chunks of the
