@@ -58,12 +58,6 @@ constexpr int kP = kChunk / 64;                // positions per lane
 // ratio 0.578 instead of 0.598 on the bench text but runs 7% slower (more copies to parse).
 constexpr uint32_t kTabBits = 13;
 constexpr uint32_t kTabBytes = 4u << kTabBits;
-// SM_FAST_T16: depth 1 uses the same 32 KiB as 16 K u16 buckets (14-bit hash), exchanged with
-// ds_mskor_rtn_b32 (a masked exchange of one half-dword; inline asm: no builtin exists)
-#ifndef SM_FAST_T16
-#define SM_FAST_T16 0
-#endif
-constexpr bool kTab16 = SM_FAST_T16;
 constexpr uint32_t kWavesPerBlock = 16;
 constexpr uint32_t kPW = kWavesPerBlock - 1;  // parse waves; wave kPW is the inserter
 constexpr uint32_t kThreads = 64 * kWavesPerBlock;
@@ -201,9 +195,8 @@ struct Cfg {
 // are all invalid too, and within one exchange the lower lanes go first).
 template <typename Cand>
 __device__ inline void hash_group(const uint8_t* data, Cand* hr, uint32_t base, uint32_t lane) {
-  constexpr uint32_t kBits = (kTab16 && sizeof(Cand) == 2) ? kTabBits + 1 : kTabBits;
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(data + base) + (lane >> 2);
-  hr[lane] = (Cand)fast_hash<kBits>(__builtin_amdgcn_alignbyte(dw[1], dw[0], lane & 3u));
+  hr[lane] = (Cand)fast_hash<kTabBits>(__builtin_amdgcn_alignbyte(dw[1], dw[0], lane & 3u));
 }
 
 // Inserter: positions [r0, r0 + kRoundPos) in order.  ring[i] holds the hash of position r0 + i
@@ -225,41 +218,10 @@ __device__ inline void insert_round(uint32_t* T, typename Cfg<D>::Cand* ring, ui
   auto step = [&](uint32_t g0, uint32_t (&h)[kG], bool guarded) {
     const uint32_t pos1 = r0 + 64 * g0 + lane + 1;
     uint32_t old[kG], hn[kG];
-    if (kTab16 && D == 1) {
-      // bucket h is half (h & 1) of dword h >> 1: D = (D & ~mask) | value, the old dword back.
-      // The six exchanges and their wait are ONE asm statement (early-clobber results), so the
-      // compiler cannot touch a result register before the data has returned; a group past the
-      // round's end exchanges with mask 0 (memory unchanged).
-      uint32_t la[kG], mk[kG], vv[kG];
 #pragma unroll
-      for (int i = 0; i < kG; ++i) {
-        const bool v = !guarded || g0 + i < ngroups;
-        const uint32_t hh = v ? h[i] : 0u, sh = (hh & 1u) << 4;
-        la[i] = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)(&T[hh >> 1]));
-        mk[i] = v ? 0xffffu << sh : 0u;
-        vv[i] = v ? (pos1 + 64 * i) << sh : 0u;
-      }
-      static_assert(kG == 6, "the asm below issues kG exchanges");
-      asm volatile(
-          "ds_mskor_rtn_b32 %0, %6, %12, %18\n"
-          "ds_mskor_rtn_b32 %1, %7, %13, %19\n"
-          "ds_mskor_rtn_b32 %2, %8, %14, %20\n"
-          "ds_mskor_rtn_b32 %3, %9, %15, %21\n"
-          "ds_mskor_rtn_b32 %4, %10, %16, %22\n"
-          "ds_mskor_rtn_b32 %5, %11, %17, %23\n"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(old[0]), "=&v"(old[1]), "=&v"(old[2]), "=&v"(old[3]), "=&v"(old[4]), "=&v"(old[5])
-          : "v"(la[0]), "v"(la[1]), "v"(la[2]), "v"(la[3]), "v"(la[4]), "v"(la[5]), "v"(mk[0]), "v"(mk[1]), "v"(mk[2]),
-            "v"(mk[3]), "v"(mk[4]), "v"(mk[5]), "v"(vv[0]), "v"(vv[1]), "v"(vv[2]), "v"(vv[3]), "v"(vv[4]), "v"(vv[5])
-          : "memory");
-#pragma unroll
-      for (int i = 0; i < kG; ++i) old[i] = (old[i] >> ((h[i] & 1u) << 4)) & 0xffffu;
-    } else {
-#pragma unroll
-      for (int i = 0; i < kG; ++i)
-        if (!guarded || g0 + i < ngroups)
-          old[i] = __hip_atomic_exchange(&T[h[i]], pos1 + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    for (int i = 0; i < kG; ++i)
+      if (!guarded || g0 + i < ngroups)
+        old[i] = __hip_atomic_exchange(&T[h[i]], pos1 + 64 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     // the next step's hashes, behind this step's exchanges
 #pragma unroll
     for (int i = 0; i < kG; ++i)
