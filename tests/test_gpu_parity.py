@@ -139,8 +139,9 @@ def test_fast_mode_batched_roundtrip(sm, oracle, libsnappy, gpu_available, corpu
     blocks = []
     for raw in corpus.values():
         blocks.extend(blocks_of(raw))
-    # sizes at the parse's chunk (256 B) and round (15 x 256 B) boundaries
-    edges = [k * m + d for m in (256, 3840) for k in (1, 2, 17) for d in (-1, 0, 1) if 0 < k * m + d <= 65536]
+    # sizes at the parse's chunk (256 B) and round (30 x 256 B fast, 15 x 256 B dense) boundaries;
+    # k = 2, 3 rounds: the prologue hashes rounds 0 and 1, the parse waves the later ones
+    edges = [k * m + d for m in (256, 3840, 7680) for k in (1, 2, 3, 17) for d in (-1, 0, 1) if 0 < k * m + d <= 65536]
     for n in list(range(0, 70)) + edges + [65535, 65536]:
         blocks.append(rng.integers(0, 3, n, dtype=np.uint8).tobytes())
     for n in edges[:6]:
