@@ -1,14 +1,10 @@
 // sm_compress.hip -- batched 64 KiB-block snappy compression for gfx950 (MI355X).
 //
-// Two kernels, one wavefront (64 lanes) per block, block staged in LDS:
-//
 //  k_compress_exact  -- "reference mode": byte-identical to Snappy.jl's compress
 //                       (src/internal.jl:127-250 incl. quirks Q1/Q3, src/Snappy.jl:20-36 incl.
-//                       Q2).  The greedy parse is inherently serial (the u16 hash table at
-//                       internal.jl:189-193 carries state between probes), so it runs as
-//                       wave-uniform scalar code; the wave parallelises what is parallel:
-//                       block staging, table reset, find_match_length (256 B compared per
-//                       LDS round, internal.jl:343-387) and literal copies.
+//                       Q2).  The greedy parse is serial, so one wave runs it per block as
+//                       wave-uniform code; five blocks share a CU (the block is read from HBM,
+//                       only the 32 KiB table is in LDS).  See "reference mode" below.
 //
 //  k_compress_fast   -- "fast mode", see sm_compress_fast.hip.
 //
@@ -24,32 +20,12 @@ __device__ unsigned long long g_stamp_x[8];
 #endif
 STAMP_MACROS(8)
 
-constexpr uint32_t kLdsPad = 64;  // readable slack after the block for lds_ld32 / wave compares
-
 // ---- output emission (global memory, wave-uniform op) -------------------------------
 
 __device__ inline uint32_t emit_varint(uint8_t* dst, uint32_t op, uint32_t v, uint32_t lane) {
   uint32_t nb = varint_len(v);
   if (lane < nb) dst[op + lane] = (uint8_t)(((v >> (7 * lane)) & 0x7f) | (lane + 1 < nb ? 0x80 : 0));
   return op + nb;
-}
-
-// internal.jl:252-287.  ref_q3: one-byte tag only for len < 60 (Snappy.jl); else len-1 < 60.
-__device__ inline uint32_t emit_literal_g(uint8_t* dst, uint32_t op, const uint8_t* lds, uint32_t start,
-                                          uint32_t len, uint32_t lane, bool ref_q3) {
-  uint32_t n = len - 1;
-  bool one = ref_q3 ? (len < 60) : (n < 60);
-  if (one) {
-    if (lane == 0) dst[op] = (uint8_t)(n << 2);
-    op += 1;
-  } else {
-    uint32_t count = n < 256 ? 1 : n < 65536 ? 2 : n < (1u << 24) ? 3 : 4;
-    if (lane == 0) dst[op] = (uint8_t)((59 + count) << 2);
-    if (lane >= 1 && lane <= count) dst[op + lane] = (uint8_t)(n >> (8 * (lane - 1)));
-    op += 1 + count;
-  }
-  wave_copy_lds_to_global(dst + op, lds, start, len, lane);
-  return op + len;
 }
 
 // internal.jl:289-304 (single lane)
@@ -73,59 +49,194 @@ __device__ inline uint32_t put_copy(uint8_t* dst, uint32_t op, uint32_t offset, 
   return put_copy_upto_64(dst, op, offset, len);
 }
 
-__device__ inline uint32_t emit_copy_g(uint8_t* dst, uint32_t op, uint32_t offset, uint32_t len, uint32_t lane) {
-  if (lane == 0) put_copy(dst, op, offset, len);
-  return op + copy_tag_bytes(offset, len);
-}
-
-__device__ inline uint32_t uld32(const uint8_t* lds, uint32_t pos) { return uniform(lds_ld32(lds, pos)); }
-
 // ---- reference mode ------------------------------------------------------------------
 //
-// Batched exact probes.  After every copy the reference's literal search probes positions
-// p0 + D[k], D[0] = 0, D[k+1] = D[k] + (skip_k >> 5), skip_0 = 32, skip_{k+1} = skip_k +
-// (skip_k >> 5) (internal.jl:162-175): a fixed sequence, so 64 probes go in one step, lane j =
-// probe k0 + j.  Probe k runs only if p0 + D[k+1] <= ip_limit (:175, checked before the probe).
-// Its candidate is the table entry as of just before it (:190), i.e. the latest earlier
-// insert with its hash.  Inserted positions only ever increase within a fragment (probes, then
-// ip-1 and ip after a copy, :228-235), so the table holds pos+1 (0 = never written, read as
-// candidate 0 exactly like the reference's 0xffff refill, Snappy.jl:30 / internal.jl:190) and
-// ds_max_rtn_u32 gives every lane its exact sequential candidate: conflicting lanes of one
-// instruction are serviced in ascending lane order on gfx950 (tools/probe_lds.hip; the
-// byte-parity tests pin it).  The first lane whose candidate matches is the reference's
-// match; the inserts of later lanes never happened sequentially and are undone exactly: for
-// each hash, the first later lane's return value is the entry's correct value.
+// The reference's greedy parse (internal.jl:127-250) is serial: the hash table carries state
+// from probe to probe (:189-193), and skip and limit depend on it.  One wave runs it per block
+// as wave-uniform code.  The kernel's speed is therefore how many parses run at once per CU,
+// times how short each parse's dependency chain is:
+//
+//  * Five parses per CU.  The block is read in place from HBM through a buffer resource
+//    (range-checked: reads past the block return 0; the block's lines stay in L2), and the
+//    only LDS is the 32 KiB table of 16 K u16 entries in the reference's own encoding,
+//    (pos - 1) mod 2^16 with 0xffff = empty = candidate 0 (Snappy.jl:30, internal.jl:190-191).
+//    Staging the block in LDS instead fits one parse per CU (1.1-2.8 GB/s measured).
+//  * Batched exact probes.  After every copy the literal search probes positions p0 + D[k],
+//    D[0] = 0, D[k+1] = D[k] + (skip_k >> 5), skip_0 = 32, skip_{k+1} = skip_k + (skip_k >> 5)
+//    (:162-175): a fixed sequence, so 64 probes go in one step, lane j = probe k0 + j.  Probe k
+//    runs only if p0 + D[k+1] <= ip_limit (:175, checked before the probe).  Its candidate is
+//    the table entry as of just before it (:190).  Each lane exchanges its half-dword entry
+//    with ds_mskor_rtn_b32; the lanes of one LDS instruction are serviced in ascending lane
+//    order on gfx950 (tools/probe_lds.hip; the byte-parity tests pin it), so every lane gets
+//    its exact sequential candidate.  The first lane whose candidate matches is the
+//    reference's match; the inserts of later lanes never happened sequentially and are undone
+//    exactly: for each hash, the first later lane's returned entry is the correct value.
+//  * Fused verification.  A copy step compares 256 bytes at cand and ip in one round; bytes
+//    [0, 4) are the reference's verification (:238), the rest find_match_length (:216).  The
+//    words at ip-1 and ip for the next step's hashes (:228-231) come out of the same round's
+//    registers (two readlanes), not from another load.
+//  * Deferred emission.  A copy is a token (position, offset, length) written into lane
+//    (copy index mod 64); every 64 copies the wave emits them together: sizes, a DPP scan for
+//    the output offsets, then each lane writes its literal run (the bytes since the previous
+//    copy; runs over 64 bytes by the whole wave) and its copy tags.  The bytes equal the
+//    reference's in-line emission (:200, :217), which depends only on the token sequence.
 
 constexpr uint32_t kMaxProbes = 320;  // D[k] > 65536 for k >= ~250: a search never gets further
+constexpr uint32_t kProbeSteps = kMaxProbes / kWave;
+constexpr uint32_t kTabBytes = 2 * kMaxHashTableSize;
+
+// The block in HBM: dword pairs through a raw buffer resource over [0, n rounded up to 4).
+struct BlockBytes {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ uint32_t word(uint32_t pos) const {
+    const int w = (int)(pos & ~3u);
+    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(r, w, 0, 0);
+    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(r, w + 4, 0, 0);
+    return __builtin_amdgcn_alignbyte(hi, lo, pos & 3u);
+  }
+  __device__ uint32_t byte(uint32_t pos) const { return __builtin_amdgcn_raw_buffer_load_b8(r, (int)pos, 0, 0); }
+};
+
+// Table entry h is half (h & 1) of dword h >> 1.  The probe's exchange and its wait are one asm
+// statement with an early-clobber result, so the compiler cannot copy the result register
+// before the data lands.  Returns the entry's old value.
+__device__ inline uint32_t tab_probe(uint32_t* t, uint32_t h, uint32_t p) {
+  const uint32_t sh = (h & 1u) << 4;
+  const uint32_t addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)(&t[h >> 1]));
+  const uint32_t mk = 0xffffu << sh, v = ((p - 1) & 0xffffu) << sh;
+  uint32_t old;
+  asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(old)
+               : "v"(addr), "v"(mk), "v"(v)
+               : "memory");
+  return (old >> sh) & 0xffffu;
+}
+__device__ inline uint32_t tab_cand(uint32_t raw) { return (raw + 1) & 0xffffu; }  // :190
+
+// wave-cooperative copy of len block bytes from s to global memory (16-byte stores in the body)
+__device__ inline void copy_to_global(const BlockBytes& S, uint8_t* __restrict__ g, uint32_t s, uint32_t len,
+                                      uint32_t lane) {
+  uint32_t head = (uint32_t)((16 - ((uintptr_t)g & 15)) & 15);
+  if (head > len) head = len;
+  if (lane < head) g[lane] = (uint8_t)S.byte(s + lane);
+  g += head; s += head; len -= head;
+  const uint32_t n16 = len >> 4;
+  uint4* g16 = reinterpret_cast<uint4*>(g);
+  for (uint32_t k = lane; k < n16; k += kWave) {
+    const uint32_t p = s + 16 * k;
+    uint4 v;
+    v.x = S.word(p);
+    v.y = S.word(p + 4);
+    v.z = S.word(p + 8);
+    v.w = S.word(p + 12);
+    g16[k] = v;
+  }
+  const uint32_t done = n16 << 4;
+  if (lane < len - done) g[done + lane] = (uint8_t)S.byte(s + done + lane);
+}
+
+// internal.jl:252-287, whole wave.  Q3: the one-byte tag only for len < 60.
+__device__ inline uint32_t emit_literal_w(const BlockBytes& S, uint8_t* dst, uint32_t op, uint32_t start,
+                                          uint32_t len, uint32_t lane) {
+  const uint32_t n = len - 1;
+  if (len < 60) {
+    if (lane == 0) dst[op] = (uint8_t)(n << 2);
+    op += 1;
+  } else {
+    const uint32_t count = n < 256 ? 1 : n < 65536 ? 2 : n < (1u << 24) ? 3 : 4;
+    if (lane == 0) dst[op] = (uint8_t)((59 + count) << 2);
+    if (lane >= 1 && lane <= count) dst[op + lane] = (uint8_t)(n >> (8 * (lane - 1)));
+    op += 1 + count;
+  }
+  copy_to_global(S, dst + op, start, len, lane);
+  return op + len;
+}
+
+// Emission of ntok (<= 64) queued copies: lane t holds copy t (tk = position | offset << 16,
+// tl = length), preceded by its literal run from the previous copy's end (`base` for t = 0).
+// Returns the new output offset; base becomes the last copy's end.
+__device__ uint32_t flush_copies(const BlockBytes& S, uint8_t* __restrict__ dst, uint32_t op, uint32_t& base,
+                                 uint32_t ntok, uint32_t tk, uint32_t tl, uint32_t lane) {
+  const bool act = lane < ntok;
+  const uint32_t pos = tk & 0xffffu, off = tk >> 16;
+  const uint32_t end = pos + tl;
+  const uint32_t pend = __shfl_up(end, 1, kWave);
+  const uint32_t ls = lane == 0 ? base : pend;
+  const uint32_t ll = act ? pos - ls : 0u;
+  // literal tag bytes, Q3 (:271-284); a run is < 65536 bytes here
+  const uint32_t lt = ll == 0 ? 0u : ll < 60 ? 1u : ll <= 256 ? 2u : 3u;
+  const uint32_t ct = act ? copy_tag_bytes(off, tl) : 0u;
+  const uint32_t sz = lt + ll + ct;
+  const uint32_t inc = scan_dpp(sz);
+  const uint32_t o = op + inc - sz;
+  const uint32_t lo = o + lt;
+  if (lt == 1) dst[o] = (uint8_t)((ll - 1) << 2);
+  if (lt > 1) {
+    const uint32_t n1 = ll - 1;
+    dst[o] = (uint8_t)((58 + lt) << 2);
+    dst[o + 1] = (uint8_t)n1;
+    if (lt > 2) dst[o + 2] = (uint8_t)(n1 >> 8);
+  }
+  for (uint32_t i = 0;; i += 4) {  // runs up to 64 bytes: lane-private, four bytes a step
+    const bool go = ll <= 64 && i < ll;
+    if (!ballot(go)) break;
+    if (go) {
+      const uint32_t w = S.word(ls + i), r = ll - i;
+      uint8_t* q = dst + lo + i;
+      q[0] = (uint8_t)w;
+      if (r > 1) q[1] = (uint8_t)(w >> 8);
+      if (r > 2) q[2] = (uint8_t)(w >> 16);
+      if (r > 3) q[3] = (uint8_t)(w >> 24);
+    }
+  }
+  for (uint64_t lm = ballot(ll > 64); lm; lm &= lm - 1) {  // longer runs: the whole wave
+    const uint32_t t = ctz64(lm);
+    copy_to_global(S, dst + readlane(lo, t), readlane(ls, t), readlane(ll, t), lane);
+  }
+  if (act) put_copy(dst, lo + ll, off, tl);
+  base = readlane(end, ntok - 1);
+  return op + readlane(inc, kWave - 1);
+}
+
+// lane l of old := v (v and l wave-uniform; no builtin for v_writelane_b32 in this compiler)
+__device__ inline uint32_t writelane(uint32_t v, uint32_t l, uint32_t old) {
+  asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(old) : "s"(v), "{m0}"(l));
+  return old;
+}
 
 __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t sdata[kBlockSize + kLdsPad];
-  __shared__ __attribute__((aligned(16))) uint32_t stab[kMaxHashTableSize];  // pos + 1, 0 = empty
-  __shared__ uint32_t sD[kMaxProbes + 1];                                     // probe offsets
+  __shared__ __attribute__((aligned(16))) uint32_t stab[kTabBytes / 4];
 
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
   const uint32_t n = a.in_len[b];
-  const uint8_t* src = a.in + a.in_off[b];
   uint8_t* dst = a.out + a.out_off[b];
-  if (n > kBlockSize) {  // batch contract violated: refuse instead of overrunning LDS
+  if (n > kBlockSize) {  // batch contract violated: refuse (positions are 16-bit)
     if (lane == 0) a.out_len[b] = 0xffffffffu;
     return;
   }
-
-  wave_load_global_to_lds(sdata, src, n, lane);
-  if (lane < kLdsPad) sdata[n + lane] = 0;
+  BlockBytes S;
+  S.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.in + a.in_off[b]), (short)0, (int)((n + 3) & ~3u),
+                                          0x00020000);
   const uint32_t tsize = a.table_size ? a.table_size : hashtable_size(n);      // Snappy.jl:27 (Q2)
   const uint32_t shift = 32 - (31 - __builtin_clz(tsize));                     // internal.jl:128
-  for (uint32_t k = lane; k < tsize; k += kWave) stab[k] = 0;                  // Snappy.jl:30
-  if (lane == 0) {
+  for (uint32_t k = lane; k < tsize / 2; k += kWave) stab[k] = 0xffffffffu;    // Snappy.jl:30
+  // probe offsets D[64 i + lane] and D[64 i + lane + 1] (:170-172), in registers
+  uint32_t Dk[kProbeSteps] = {}, Dn[kProbeSteps] = {};
+  {
     uint32_t d = 0, skip = 32;
-    for (uint32_t k = 0; k <= kMaxProbes; ++k) {
-      sD[k] = d;
-      const uint32_t step = skip >> 5;                                         // :170-172
-      skip += step;
-      d = min(d + step, 0x20000u);
+#pragma unroll
+    for (uint32_t i = 0; i < kProbeSteps; ++i) {
+      for (uint32_t l = 0; l < kWave; ++l) {
+        Dk[i] = writelane(d, l, Dk[i]);
+        if (l) Dn[i] = writelane(d, l - 1, Dn[i]);
+        else if (i) Dn[i - 1] = writelane(d, kWave - 1, Dn[i - 1]);
+        const uint32_t step = skip >> 5;
+        skip += step;
+        d = min(d + step, 0x20000u);
+      }
     }
+    Dn[kProbeSteps - 1] = writelane(d, kWave - 1, Dn[kProbeSteps - 1]);
   }
   __syncthreads();
 
@@ -136,30 +247,34 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
   }
   const uint32_t e = n - 1;                  // inclusive end (ip_end)
   const int32_t ip_limit = (int32_t)n - 16;  // internal.jl:131, Q1: 1-based ip_end-15
-  uint32_t ip = 0, next_emit = 0, cand = 0;
-
+  uint32_t ip = 0, next_emit = 0, base = 0, ntok = 0, tk = 0, tl = 0;
   STAMP_DECL
+
   if (n >= kInputMarginBytes) {                                                // internal.jl:133
     for (;;) {
       STAMP(4)
       ip += 1;                                                                 // :163
       // literal search, 64 probes per step (:167-194)
       const uint32_t p0 = ip;
+      uint32_t cand = 0;
       bool found = false;
-      for (uint32_t k0 = 0; k0 < kMaxProbes; k0 += kWave) {
-        const uint32_t p = p0 + sD[k0 + lane];
-        const bool valid = (int32_t)(p0 + sD[k0 + lane + 1]) <= ip_limit;     // :175
-        const uint32_t cur = valid ? lds_ld32(sdata, p) : 0u;
+#pragma unroll
+      for (uint32_t i = 0; i < kProbeSteps; ++i) {
+        STAMP_COUNT(7, 1)
+        const uint32_t p = p0 + Dk[i];
+        const bool valid = (int32_t)(p0 + Dn[i]) <= ip_limit;                 // :175
+        const uint32_t cur = S.word(p);
         const uint32_t h = hash32(cur, shift);
-        uint32_t r = 0;
-        if (valid) r = __hip_atomic_fetch_max(&stab[h], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const uint32_t c = r ? r - 1 : 0u;                                     // :190
-        const bool hit = valid && lds_ld32(sdata, c) == cur;                   // :193
+        uint32_t raw = 0;
+        if (valid) raw = tab_probe(stab, h, p);
+        const uint32_t c = tab_cand(raw);
+        const bool hit = valid && S.word(c) == cur;                            // :193
         const uint64_t hm = ballot(hit);
         if (hm) {
           const uint32_t j = ctz64(hm);
           const uint32_t pj = readlane(p, j);
-          if (valid && lane > j && r <= pj + 1) stab[h] = r;                   // undo later probes
+          if (valid && lane > j && c <= pj)                                    // undo later probes
+            reinterpret_cast<uint16_t*>(stab)[h] = (uint16_t)raw;
           ip = pj;
           cand = readlane(c, j);
           found = true;
@@ -169,34 +284,67 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
       }
       STAMP(0)
       if (!found) goto emit_remainder;
-      op = emit_literal_g(dst, op, sdata, next_emit, ip - next_emit, lane, true);   // :200
-      STAMP(1)
       for (;;) {                                                               // :211-239
-        STAMP_COUNT(6, 1)
-        uint32_t avail = e - (ip + 4) + 1;
-        uint32_t matched = 4 + wave_match_length(sdata, cand + 4, ip + 4, avail, lane);  // :216
-        STAMP(2)
-        op = emit_copy_g(dst, op, ip - cand, matched, lane);                   // :217
-        ip += matched;
-        next_emit = ip;
-        if ((int32_t)ip >= ip_limit) goto emit_remainder;                      // :222
-        uint32_t prev_hash = hash32(uld32(sdata, ip - 1), shift);              // :228
-        uint32_t input_bytes = uld32(sdata, ip);
-        uint32_t cur_hash = hash32(input_bytes, shift);
-        if (lane == 0) stab[prev_hash] = ip;                                   // :233 (pos ip-1)
-        const uint32_t rv = uniform(stab[cur_hash]);                           // :234
-        cand = rv ? rv - 1 : 0u;
-        if (lane == 0) stab[cur_hash] = ip + 1;                                // :235 (pos ip)
-        if (input_bytes != uld32(sdata, cand)) {                               // :238
-          STAMP(3)
-          break;
+        // bytes [0, 4) of a round are the verification (:238; known equal after a probe hit),
+        // the rest find_match_length (:216).  Reads past the block return 0 and are capped.
+        const uint32_t avail = n - ip;
+        uint32_t f, A, rb = 0;
+        for (;;) {
+          const uint32_t off = rb + 4 * lane;
+          A = S.word(ip + off);
+          const uint32_t x = A ^ S.word(cand + off);
+          const uint32_t fb = x ? (uint32_t)(__builtin_ctz(x) >> 3) : 4u;
+          const uint64_t m = ballot(fb < 4 || off + 4 >= avail);
+          if (m) {
+            f = min(readlane(off + fb, ctz64(m)), avail);
+            break;
+          }
+          rb += 4 * kWave;
         }
+        STAMP(2)
+        if (f < 4) break;                                                      // :238
+        STAMP_COUNT(6, 1)
+        tk = writelane(ip | ((ip - cand) << 16), ntok, tk);
+        tl = writelane(f, ntok, tl);
+        ++ntok;
+        const bool inreg = rb == 0 && f <= 4 * kWave - 4;
+        uint32_t wp = 0, wc = 0;
+        if (inreg) {  // the words at ip+f-1 and ip+f, from lanes (f-1)/4 and (f-1)/4 + 1
+          const uint32_t k = (f - 1) >> 2, r8 = ((f - 1) & 3u) << 3;
+          const uint64_t w = ((uint64_t)readlane(A, k + 1) << 32) | readlane(A, k);
+          wp = (uint32_t)(w >> r8);
+          wc = (uint32_t)(w >> (r8 + 8));
+        }
+        ip += f;                                                               // :217-220
+        next_emit = ip;
+        if (ntok == kWave) {
+          STAMP(3)
+          op = flush_copies(S, dst, op, base, ntok, tk, tl, lane);
+          ntok = 0;
+          STAMP(1)
+        }
+        if ((int32_t)ip >= ip_limit) goto emit_remainder;                      // :222
+        if (!inreg) {
+          wp = uniform(S.word(ip - 1));
+          wc = uniform(S.word(ip));
+        }
+        // :228-235, one lane: insert ip-1, then read and replace the entry for ip
+        uint32_t raw = 0;
+        if (lane == 0) {
+          uint16_t* u = reinterpret_cast<uint16_t*>(stab);
+          u[hash32(wp, shift)] = (uint16_t)(ip - 2);
+          const uint32_t h2 = hash32(wc, shift);
+          raw = u[h2];
+          u[h2] = (uint16_t)(ip - 1);
+        }
+        cand = tab_cand(readlane(raw, 0));
         STAMP(3)
       }
     }
   }
 emit_remainder:
-  if (next_emit <= e) op = emit_literal_g(dst, op, sdata, next_emit, e - next_emit + 1, lane, true);  // :244-248
+  if (ntok) op = flush_copies(S, dst, op, base, ntok, tk, tl, lane);
+  if (next_emit <= e) op = emit_literal_w(S, dst, op, next_emit, e - next_emit + 1, lane);  // :244-248
   STAMP(5)
   STAMP_FLUSH(g_stamp_x)
   if (lane == 0) a.out_len[b] = op;

@@ -96,7 +96,7 @@ def compress_stamps(args):
           " ".join("%d" % (v[12 + w] / max(irounds, 1)) for w in range(16)))
 
 
-XNAMES = ["search", "literal emit", "match length", "emit+hash+table+verify", "loop top", "remainder"]
+XNAMES = ["search", "flush (emission)", "copy round", "token+hash+table", "loop top", "remainder"]
 
 
 def exact_stamps(args):
@@ -116,7 +116,8 @@ def exact_stamps(args):
     v = list(buf)
     copies = v[6]
     tot = sum(v[:6])
-    print("compress_ref %s: %d copy steps (%.0f per block)" % (args.data, copies, copies / args.blocks))
+    print("compress_ref %s: %d copy steps (%.0f per block), %d probe steps (%.0f per block)" % (
+        args.data, copies, copies / args.blocks, v[7], v[7] / args.blocks))
     for i, nme in enumerate(XNAMES):
         print("  %-24s %5.1f%%  %7.0f cycles/copy" % (nme, 100.0 * v[i] / tot, v[i] / max(copies, 1)))
 
