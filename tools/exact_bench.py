@@ -29,6 +29,9 @@ def main():
         clen = b.comp_len.cpu().numpy().astype(np.uint32)
         comp = b.d_comp.cpu().numpy()
         n = min(args.check, args.blocks)
+        if n == 0:
+            print("%s: %.3f ms  %.3f GB/s" % (kind, ms, args.blocks * bench.BLOCK / (ms * 1e-3) / 1e9), flush=True)
+            continue
         inp = np.ascontiguousarray(blocks[:n]).reshape(-1)
         o_comp = np.zeros(n * bench.SLOT, dtype=np.uint8)
         o_len = np.zeros(n, dtype=np.uint32)
