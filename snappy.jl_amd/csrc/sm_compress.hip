@@ -57,7 +57,7 @@ __device__ inline uint32_t put_copy(uint8_t* dst, uint32_t op, uint32_t offset, 
 // times how short each parse's dependency chain is:
 //
 //  * Five parses per CU.  The block is read in place from HBM through a buffer resource
-//    (range-checked: reads past the block return 0; the block's lines stay in L2), and the
+//    (range-checked to exactly the block; its lines stay in L2), and the
 //    only LDS is the 32 KiB table of 16 K u16 entries in the reference's own encoding,
 //    (pos - 1) mod 2^16 with 0xffff = empty = candidate 0 (Snappy.jl:30, internal.jl:190-191).
 //    Staging the block in LDS instead fits one parse per CU (1.1-2.8 GB/s measured).
@@ -85,14 +85,17 @@ constexpr uint32_t kMaxProbes = 320;  // D[k] > 65536 for k >= ~250: a search ne
 constexpr uint32_t kProbeSteps = kMaxProbes / kWave;
 constexpr uint32_t kTabBytes = 2 * kMaxHashTableSize;
 
-// The block in HBM: dword pairs through a raw buffer resource over [0, n rounded up to 4).
+// The block in HBM through a raw buffer resource over exactly [0, n): a dword load at offset o
+// returns 0 when o + 4 > n (the whole dword; measured on gfx950, tools/probes/buffer_range.hip), and unaligned
+// dword loads are served.  word(pos) therefore loads at min(pos, n - 4) and shifts, so the
+// bytes below n are exact and the bytes past it read 0 (the zero slack the reference's
+// find_match_length never compares) -- and no load touches memory past the block.
 struct BlockBytes {
   __amdgpu_buffer_rsrc_t r;
+  uint32_t nm4;  // n - 4 (word() is used only when n >= 15)
   __device__ uint32_t word(uint32_t pos) const {
-    const int w = (int)(pos & ~3u);
-    const uint32_t lo = __builtin_amdgcn_raw_buffer_load_b32(r, w, 0, 0);
-    const uint32_t hi = __builtin_amdgcn_raw_buffer_load_b32(r, w + 4, 0, 0);
-    return __builtin_amdgcn_alignbyte(hi, lo, pos & 3u);
+    const uint32_t pc = min(pos, nm4);
+    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)pc, 0, 0) >> ((pos - pc) << 3);
   }
   __device__ uint32_t byte(uint32_t pos) const { return __builtin_amdgcn_raw_buffer_load_b8(r, (int)pos, 0, 0); }
 };
@@ -216,8 +219,8 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
     return;
   }
   BlockBytes S;
-  S.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.in + a.in_off[b]), (short)0, (int)((n + 3) & ~3u),
-                                          0x00020000);
+  S.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.in + a.in_off[b]), (short)0, (int)n, 0x00020000);
+  S.nm4 = n - 4;
   const uint32_t tsize = a.table_size ? a.table_size : hashtable_size(n);      // Snappy.jl:27 (Q2)
   const uint32_t shift = 32 - (31 - __builtin_clz(tsize));                     // internal.jl:128
   for (uint32_t k = lane; k < tsize / 2; k += kWave) stab[k] = 0xffffffffu;    // Snappy.jl:30

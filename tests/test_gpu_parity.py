@@ -109,6 +109,31 @@ def test_reference_mode_fragments_device(sm, oracle, gpu_available):
     assert oracle.encode32(total) + b"".join(frags) == oracle.compress(raw)
 
 
+def test_reference_mode_block_end_exact(sm, oracle, gpu_available):
+    """k_compress_exact reads the block in place through a buffer resource bounded at exactly
+    n bytes: matches that run to the block's last byte, blocks of every length mod 4, at every
+    address mod 4, with the block ending at the end of the device tensor."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(17)
+    for n in (65536, 65535, 65534, 65533, 4099, 1029, 31):
+        for lead in (0, 1, 2, 3):
+            pat = rng.integers(0, 256, 7, dtype=np.uint8).tobytes()
+            head = rng.integers(0, 256, n // 3, dtype=np.uint8).tobytes()
+            blk = (head + pat * (n // 7 + 1))[:n]  # a run of copies to the very end
+            buf = bytes(lead) + blk
+            d_in = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to(dev)
+            d_off = torch.tensor([lead], dtype=torch.int64, device=dev)
+            d_len = torch.tensor([n], dtype=torch.int32, device=dev)
+            d_out = torch.empty(76496, dtype=torch.uint8, device=dev)
+            d_ooff = torch.zeros(1, dtype=torch.int64, device=dev)
+            d_olen = torch.zeros(1, dtype=torch.int32, device=dev)
+            sm.compress_batch_device(d_in, d_off, d_len, d_out, d_ooff, d_olen, mode="reference")
+            torch.cuda.synchronize()
+            out = d_out[:int(d_olen.item())].cpu().numpy().tobytes()
+            assert out == oracle.compress(blk), (n, lead)
+
+
 # ---- fast mode --------------------------------------------------------------------------
 
 FAST_MODES = ["fast", "dense"]
