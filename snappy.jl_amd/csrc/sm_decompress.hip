@@ -51,6 +51,14 @@ typedef uint16_t __attribute__((aligned(1))) du16u;
 typedef uint32_t __attribute__((aligned(1))) du32u;
 typedef uint64_t __attribute__((aligned(1))) du64u;
 
+// 8 bytes of earlier output at p for a far copy source (its destination starts at lim >= p + 1,
+// lim >= 8): the load never reaches lim -- the stream (and the caller's buffer) may end a few
+// bytes after it -- and the bytes at or past lim, which the copy masks off anyway, read as 0.
+__device__ inline uint64_t out_get8(const uint8_t* out, uint32_t p, uint32_t lim) {
+  const uint32_t a = min(p, lim - 8);
+  return *reinterpret_cast<const du64u*>(out + a) >> (8 * (p - a));
+}
+
 constexpr uint32_t kRing = 1024;
 constexpr uint32_t kMaxBatchLit = 200;  // longer literals stop a window walk (size 255)
 constexpr int kWalkLevels = 5;  // tables J0..J4 in LDS; J5 (bit 5 of a lane's chain index) = J4 o J4
@@ -391,63 +399,74 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         const bool ready = !((done >> lane) & 1) && ((SM_ABLATE_D & 2) || !iscopy || shi <= O0);
         const uint64_t rm = ballot(ready);
         const uint32_t L = iscopy ? len : litlen;
-        for (uint32_t base = 0; base < 64; base += 8 * kPass) {
-          const bool act = ready && L > base;
-          if (!ballot(act)) break;
-          if (act) {
-            uint64_t v[kPass];
-            if (!iscopy || offset >= 8) {
-              // a literal (input ring; it never wraps) or a copy with offset >= 8 (output window,
-              // or HBM for far sources): 8-byte pieces of S, wrapping once to S's start
-              const uint8_t* bb = iscopy ? win : ring;
-              const uint32_t msk = iscopy ? kWin - 1 : kRing - 1;
-              const uint32_t sp = iscopy ? slo : lsrc;
-              const uint32_t off = iscopy ? offset : 0xffffu;
-              // S's first 8 bytes, needed only when S wraps inside this pass (offset < base + 16)
-              uint64_t B = 0;
-              if (off < base + 8 * kPass) B = gsrc ? *reinterpret_cast<const du64u*>(out + slo) : lds_get8w(bb, msk, sp);
-              uint32_t m0 = base;
-              while (m0 >= off) m0 -= off;
-              uint32_t m = m0;
+        // HBM sources near the stream's end (a copy to its last 8 bytes) are read through
+        // out_get8, which stops at the copy's destination; every other batch keeps plain loads
+        const bool gtail = ballot(ready && gsrc && opt + 8 > size) != 0;
+        auto rounds = [&](auto tailc) {
+          auto gload = [&](uint32_t p) -> uint64_t {
+            if constexpr (decltype(tailc)::value) return out_get8(out, p, opt);
+            else return *reinterpret_cast<const du64u*>(out + p);
+          };
+          for (uint32_t base = 0; base < 64; base += 8 * kPass) {
+            const bool act = ready && L > base;
+            if (!ballot(act)) break;
+            if (act) {
+              uint64_t v[kPass];
+              if (!iscopy || offset >= 8) {
+                // a literal (input ring; it never wraps) or a copy with offset >= 8 (output window,
+                // or HBM for far sources): 8-byte pieces of S, wrapping once to S's start
+                const uint8_t* bb = iscopy ? win : ring;
+                const uint32_t msk = iscopy ? kWin - 1 : kRing - 1;
+                const uint32_t sp = iscopy ? slo : lsrc;
+                const uint32_t off = iscopy ? offset : 0xffffu;
+                // S's first 8 bytes, needed only when S wraps inside this pass (offset < base + 16)
+                uint64_t B = 0;
+                if (off < base + 8 * kPass) B = gsrc ? gload(slo) : lds_get8w(bb, msk, sp);
+                uint32_t m0 = base;
+                while (m0 >= off) m0 -= off;
+                uint32_t m = m0;
 #pragma unroll
-              for (int i = 0; i < kPass; ++i) {
-                v[i] = base + 8 * i < L ? (gsrc ? *reinterpret_cast<const du64u*>(out + slo + m) : lds_get8w(bb, msk, sp + m))
-                                        : 0ull;
-                m += 8;
-                if (m >= off) m -= off;
-              }
-              m = m0;
+                for (int i = 0; i < kPass; ++i) {
+                  v[i] = base + 8 * i < L ? (gsrc ? gload(slo + m) : lds_get8w(bb, msk, sp + m))
+                                          : 0ull;
+                  m += 8;
+                  if (m >= off) m -= off;
+                }
+                m = m0;
 #pragma unroll
-              for (int i = 0; i < kPass; ++i) {
-                const uint32_t keep = off - m;  // bytes of this chunk before S wraps
-                if (keep < 8) v[i] = (v[i] & ((1ull << (8 * keep)) - 1)) | (B << (8 * keep));
-                m += 8;
-                if (m >= off) m -= off;
-              }
-            } else {
-              const uint64_t x = win_get8(win, slo);
-              uint64_t p0 = x & ((1ull << (8 * offset)) - 1);
-              for (uint32_t have = offset; have < 8; have *= 2) p0 |= p0 << (8 * have);
-              // p0 = S repeated over 8 bytes; p1 = the next 8 bytes of the period
-              uint32_t e = 8;
-              while (e >= offset) e -= offset;
-              // p1[k] = seq[8+k] = p0[e+k] (e+k < 8) or p0[e+k-offset] (e+k >= 8)
-              const uint64_t hib = e ? ~0ull << (8 * (8 - e)) : 0ull;
-              const uint64_t p1 = e ? ((p0 >> (8 * e)) | ((p0 << (8 * (offset - e))) & hib)) : p0;
-              uint32_t m = base;
-              while (m >= offset) m -= offset;
-#pragma unroll
-              for (int i = 0; i < kPass; ++i) {
-                v[i] = m ? ((p0 >> (8 * m)) | (p1 << (8 * (8 - m)))) : p0;
-                m += 8;
+                for (int i = 0; i < kPass; ++i) {
+                  const uint32_t keep = off - m;  // bytes of this chunk before S wraps
+                  if (keep < 8) v[i] = (v[i] & ((1ull << (8 * keep)) - 1)) | (B << (8 * keep));
+                  m += 8;
+                  if (m >= off) m -= off;
+                }
+              } else {
+                const uint64_t x = win_get8(win, slo);
+                uint64_t p0 = x & ((1ull << (8 * offset)) - 1);
+                for (uint32_t have = offset; have < 8; have *= 2) p0 |= p0 << (8 * have);
+                // p0 = S repeated over 8 bytes; p1 = the next 8 bytes of the period
+                uint32_t e = 8;
+                while (e >= offset) e -= offset;
+                // p1[k] = seq[8+k] = p0[e+k] (e+k < 8) or p0[e+k-offset] (e+k >= 8)
+                const uint64_t hib = e ? ~0ull << (8 * (8 - e)) : 0ull;
+                const uint64_t p1 = e ? ((p0 >> (8 * e)) | ((p0 << (8 * (offset - e))) & hib)) : p0;
+                uint32_t m = base;
                 while (m >= offset) m -= offset;
-              }
-            }
 #pragma unroll
-            for (int i = 0; i < kPass; ++i)
-              if (base + 8 * i < L) win_put8(win, opt + base + 8 * i, v[i], min(8u, L - base - 8 * i));
+                for (int i = 0; i < kPass; ++i) {
+                  v[i] = m ? ((p0 >> (8 * m)) | (p1 << (8 * (8 - m)))) : p0;
+                  m += 8;
+                  while (m >= offset) m -= offset;
+                }
+              }
+#pragma unroll
+              for (int i = 0; i < kPass; ++i)
+                if (base + 8 * i < L) win_put8(win, opt + base + 8 * i, v[i], min(8u, L - base - 8 * i));
+            }
           }
-        }
+        };
+        if (gtail) rounds(std::true_type{});
+        else rounds(std::false_type{});
         done |= rm;
       }
       STAMP(8)
@@ -584,7 +603,7 @@ __device__ inline int32_t parse_header(const uint8_t* in, uint32_t N, uint32_t l
 }
 
 #ifndef SM_DEC_OCC
-#define SM_DEC_OCC 7  // waves per SIMD: 72 VGPRs (2 spilled), 4.7 KB LDS per wave
+#define SM_DEC_OCC 7  // waves per SIMD: 68 VGPRs, 4.7 KB LDS per wave
 #endif
 __global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
