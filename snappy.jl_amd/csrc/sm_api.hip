@@ -41,21 +41,32 @@ struct DevBuf {
   }
 };
 
-struct HostBuf {  // pinned host staging (one D2H transfer per batch call)
+// Host staging: page-aligned ordinary memory registered for DMA (hipHostRegister), so the CPU
+// reads it through its caches -- the host walks the index records and scatters batch outputs
+// from it.  (hipHostMalloc'd staging was read ~2x slower by those CPU loops.)
+struct HostBuf {
   void* p = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
-    size_t want = n < (1u << 20) ? (1u << 20) : n;
-    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
-    if (e == hipSuccess) cap = want;
-    return e;
+    release();
+    const size_t want = ((n < (1u << 20) ? (1u << 20) : n) + 4095) & ~(size_t)4095;
+    void* q = nullptr;
+    if (posix_memalign(&q, 4096, want) != 0) return hipErrorOutOfMemory;
+    const hipError_t e = hipHostRegister(q, want, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+      free(q);
+      return e;
+    }
+    p = q;
+    cap = want;
+    return hipSuccess;
   }
   void release() {
-    if (p) (void)hipHostFree(p);
+    if (p) {
+      (void)hipHostUnregister(p);
+      free(p);
+    }
     p = nullptr;
     cap = 0;
   }
@@ -64,6 +75,8 @@ struct HostBuf {  // pinned host staging (one D2H transfer per batch call)
 struct sm_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t copy = nullptr;     // host->device copies that overlap the kernels (sm_compress)
+  std::vector<hipEvent_t> ev;     // their completion events
   DevBuf in, out, out2, meta, idx, gat, org;  // org: origin pointers of the general parallel decode
   HostBuf stage;
   int last_path = -1;  // sm_ctx_last_path
@@ -88,7 +101,50 @@ struct DeviceGuard {
 
 inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
+#ifdef SM_HOST_TRACE  // diagnostic builds: phase times of the single-buffer entry points on stderr
+#include <chrono>
+#include <cstdio>
+struct HostTrace {
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void mark(const char* what, hipStream_t s) {
+    (void)hipStreamSynchronize(s);
+    const auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "  %-28s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(now - t).count());
+    t = now;
+  }
+};
+#define HT_DECL HostTrace ht_;
+#define HT(what) ht_.mark(what, s);
+#else
+#define HT_DECL
+#define HT(what)
+#endif
+
 constexpr uint32_t kParallelMinOutput = 4 * 65536;  // smaller streams: one wave is as fast
+constexpr size_t kPipeMinInput = 32u << 20;  // sm_compress: inputs this large upload in pieces
+constexpr uint32_t kPieceFrags = 256;        // 16 MiB per piece
+#ifndef SM_OUT_PIECE
+#define SM_OUT_PIECE 2048
+#endif
+constexpr uint32_t kOutPieceFrags = SM_OUT_PIECE;  // sm_uncompress: output pieces (128 MiB)
+
+// the context's copy stream and at least n events (created on first use)
+hipError_t ensure_copy_stream(sm_ctx* ctx, size_t n) {
+  if (!ctx->copy) {
+    const hipError_t e = hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      ctx->copy = nullptr;
+      return e;
+    }
+  }
+  while (ctx->ev.size() < n) {
+    hipEvent_t e;
+    const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+    if (r != hipSuccess) return r;
+    ctx->ev.push_back(e);
+  }
+  return hipSuccess;
+}
 
 // Host tag walk over [p, lim) of a stream (zero-padded lookahead, internal.jl:426-462): where it
 // leaves the range and how much output the tags make.  Used when a chunk is entered deeper than
@@ -118,7 +174,11 @@ void host_walk(const uint8_t* comp, uint32_t n, uint64_t p, uint64_t lim, uint64
 // One large stream in parallel (sm_decompress.hip, "one large stream"): index pass, true path
 // on the host, one wave per 64 KiB fragment.  The compressed bytes are in ctx->in.  Returns
 // 1 with the output in ctx->out, 0 to fall back to the in-order decode, -1 on a device error.
-int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t ip0, uint32_t size) {
+// With host_out, a large output goes down in pieces on the copy stream as the fragment decode
+// finishes them (*copied = true: host_out holds the result when 1 is returned).
+int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t ip0, uint32_t size,
+                        uint8_t* host_out, bool* copied) {
+  *copied = false;
   using sm::kIdxChunk;
   using sm::kIdxEntries;
   const uint32_t nchunks = (n - ip0 + kIdxChunk - 1) / kIdxChunk;
@@ -128,25 +188,33 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   const size_t st_off = frag_off + (size_t)nfrag * sizeof(sm::StreamFrag);
   if (ctx->idx.ensure(st_off + (size_t)nfrag * 4) != hipSuccess) return -1;
   hipStream_t s = ctx->stream;
-  uint32_t* d_exit = (uint32_t*)ctx->idx.p;
-  uint32_t* d_out = d_exit + rec_n;
+  HT_DECL
+  uint32_t* d_rec = (uint32_t*)ctx->idx.p;
   const uint8_t* d_in = (const uint8_t*)ctx->in.p;
-  if (sm::launch_stream_index(d_in, n, ip0, nchunks, d_exit, d_out, s) != hipSuccess) return -1;
-  std::vector<uint32_t> rec(2 * rec_n);
-  if (hipMemcpyAsync(rec.data(), d_exit, 2 * rec_n * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (sm::launch_stream_index(d_in, n, ip0, nchunks, d_rec, s) != hipSuccess) return -1;
+  HT("index kernel")
+  // the index records (8 B per entry, ~9 MB per 64 MiB of stream) come back through the
+  // context's pinned staging: one DMA, no page faults, no zero fill
+  if (ctx->stage.ensure(2 * rec_n * 4) != hipSuccess) return -1;
+  const uint32_t* rec = (const uint32_t*)ctx->stage.p;
+  if (hipMemcpyAsync(ctx->stage.p, d_rec, 2 * rec_n * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  HT("index records D2H")
   // true path: chunk entries y, output before them O, output of their tags
   struct PathChunk {
     uint64_t y, O, out, ex;
   };
   std::vector<PathChunk> path;
+  path.reserve(nchunks + 16);
   uint64_t y = ip0, O = 0;
   while (y < (uint64_t)n - 1) {  // internal.jl:416
     const uint64_t c = (y - ip0) / kIdxChunk, base = ip0 + c * kIdxChunk, l = y - base;
+    // the walk enters a chunk a few bytes in: the head of a record a few chunks ahead
+    if (c + 8 < nchunks) __builtin_prefetch(&rec[2 * (c + 8) * kIdxEntries]);
     uint64_t ex, ot;
     if (l < kIdxEntries) {
-      ex = rec[c * kIdxEntries + l];
-      ot = rec[rec_n + c * kIdxEntries + l];
+      ex = rec[2 * (c * kIdxEntries + l)];
+      ot = rec[2 * (c * kIdxEntries + l) + 1];
     } else {
       host_walk(comp, n, y, std::min<uint64_t>(base + kIdxChunk, (uint64_t)n - 1), &ex, &ot);
     }
@@ -164,22 +232,42 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
     frags[f] = {(uint32_t)path[k].y, (uint32_t)path[k].O, (uint32_t)F,
                 f + 1 == nfrag ? 0xffffffffu : (uint32_t)(F + 65536)};
   }
+  HT("host path + fragments")
   sm::StreamFrag* d_frags = (sm::StreamFrag*)((uint8_t*)ctx->idx.p + frag_off);
   int32_t* d_st = (int32_t*)((uint8_t*)ctx->idx.p + st_off);
   if (hipMemcpyAsync(d_frags, frags.data(), frags.size() * sizeof(sm::StreamFrag), hipMemcpyHostToDevice, s) !=
       hipSuccess)
     return -1;
-  if (sm::launch_decompress_frags(d_in, n, size, (uint8_t*)ctx->out.p, d_frags, nfrag, d_st, s) != hipSuccess)
-    return -1;
+  const uint32_t nfp = (nfrag + kOutPieceFrags - 1) / kOutPieceFrags;
+  const uint32_t npiece = (host_out && nfp > 1 && ensure_copy_stream(ctx, nfp) == hipSuccess) ? nfp : 1;
+  uint8_t* out = (uint8_t*)ctx->out.p;
+  for (uint32_t pc = 0; pc < npiece; ++pc) {
+    const uint32_t f0 = pc * kOutPieceFrags, f1 = npiece == 1 ? nfrag : std::min(nfrag, f0 + kOutPieceFrags);
+    if (sm::launch_decompress_frags(d_in, n, size, out, d_frags + f0, f1 - f0, d_st + f0, s) != hipSuccess) return -1;
+    if (npiece > 1 && hipEventRecord(ctx->ev[pc], s) != hipSuccess) return -1;
+  }
+  if (npiece > 1) {  // each piece's output goes down while the later pieces decode
+    for (uint32_t pc = 0; pc < npiece; ++pc) {
+      const size_t b0 = (size_t)pc * kOutPieceFrags * 65536;
+      const size_t b1 = std::min((size_t)size, b0 + (size_t)kOutPieceFrags * 65536);
+      if (hipStreamWaitEvent(ctx->copy, ctx->ev[pc], 0) != hipSuccess) return -1;
+      if (hipMemcpyAsync(host_out + b0, out + b0, b1 - b0, hipMemcpyDeviceToHost, ctx->copy) != hipSuccess) return -1;
+    }
+    if (hipStreamSynchronize(ctx->copy) != hipSuccess) return -1;
+  }
   std::vector<int32_t> st(nfrag);
   if (hipMemcpyAsync(st.data(), d_st, nfrag * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  HT("fragment decode")
   bool cross = false;
   for (int32_t v : st) {
     if (v == sm::kErrCross) cross = true;
     else if (v != sm::kOk) return 0;  // an error: the in-order decode reports it exactly
   }
-  if (!cross) return 1;
+  if (!cross) {
+    *copied = npiece > 1;
+    return 1;
+  }
   // Not block-structured (a copy reaches into an earlier block): origin pointers per output
   // byte, resolved by pointer jumping (sm_decompress.hip, "any large stream").
   if (n >= 0x80000000u || size >= 0x80000000u) return 0;  // 31-bit positions
@@ -429,6 +517,11 @@ void sm_ctx_destroy(sm_ctx* ctx) {
     ctx->gat.release();
     ctx->org.release();
     ctx->stage.release();
+    if (ctx->copy) {
+      (void)hipStreamSynchronize(ctx->copy);
+      (void)hipStreamDestroy(ctx->copy);
+    }
+    for (hipEvent_t e : ctx->ev) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
   }
   delete ctx;
@@ -673,15 +766,32 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   uint64_t* d_dst_off = (uint64_t*)(m + 16 * (size_t)nfrag);
   uint32_t* d_in_len = (uint32_t*)(m + 24 * (size_t)nfrag);
   uint32_t* d_out_len = (uint32_t*)(m + 28 * (size_t)nfrag);
-  SM_CHECK(hipMemcpyAsync(ctx->in.p, input, n, hipMemcpyHostToDevice, s));
+  HT_DECL
   SM_CHECK(hipMemcpyAsync(d_in_off, in_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
   SM_CHECK(hipMemcpyAsync(d_out_off, out_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
   SM_CHECK(hipMemcpyAsync(d_in_len, in_len.data(), 4 * (size_t)nfrag, hipMemcpyHostToDevice, s));
-  sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
-                     nfrag, sm::hashtable_size(n), 0};
-  SM_CHECK(sm::launch_compress(a, mode, s));
+  // Large inputs go up in pieces on the copy stream, and each piece's fragments compress as
+  // soon as it lands, so the kernels run under the rest of the upload.
+  const uint32_t npiece = n >= kPipeMinInput ? (nfrag + kPieceFrags - 1) / kPieceFrags : 1;
+  if (npiece > 1) SM_CHECK(ensure_copy_stream(ctx, npiece));
+  for (uint32_t pc = 0; pc < npiece; ++pc) {
+    const uint32_t f0 = pc * kPieceFrags, f1 = npiece == 1 ? nfrag : std::min(nfrag, f0 + kPieceFrags);
+    const size_t b0 = (size_t)f0 * SM_BLOCK_SIZE, b1 = std::min(n, (size_t)f1 * SM_BLOCK_SIZE);
+    if (npiece == 1) {
+      SM_CHECK(hipMemcpyAsync(ctx->in.p, input, n, hipMemcpyHostToDevice, s));
+    } else {
+      SM_CHECK(hipMemcpyAsync((uint8_t*)ctx->in.p + b0, input + b0, b1 - b0, hipMemcpyHostToDevice, ctx->copy));
+      SM_CHECK(hipEventRecord(ctx->ev[pc], ctx->copy));
+      SM_CHECK(hipStreamWaitEvent(s, ctx->ev[pc], 0));
+    }
+    sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off + f0, d_in_len + f0, (uint8_t*)ctx->out.p,
+                       d_out_off + f0, d_out_len + f0, f1 - f0, sm::hashtable_size(n), 0};
+    SM_CHECK(sm::launch_compress(a, mode, s));
+  }
+  HT("compress: H2D input + kernels")
   SM_CHECK(hipMemcpyAsync(out_len.data(), d_out_len, 4 * (size_t)nfrag, hipMemcpyDeviceToHost, s));
   SM_CHECK(hipStreamSynchronize(s));
+  HT("compress: kernels + lengths")
   size_t total = 0;
   for (uint32_t i = 0; i < nfrag; ++i) {
     dst_off[i] = total;
@@ -691,8 +801,10 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   SM_CHECK(hipMemcpyAsync(d_dst_off, dst_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
   SM_CHECK(sm::launch_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_dst_off, (uint8_t*)ctx->out2.p,
                              nfrag, s));
+  HT("compress: gather")
   SM_CHECK(hipMemcpyAsync(compressed + hl, ctx->out2.p, total, hipMemcpyDeviceToHost, s));
   SM_CHECK(hipStreamSynchronize(s));
+  HT("compress: D2H output")
   *compressed_length = hl + total;
   return SM_OK;
 }
@@ -722,18 +834,25 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   int32_t* d_status = (int32_t*)(m + 20);
   uint32_t hv[2] = {(uint32_t)n, size};
   uint64_t zero = 0;
+  HT_DECL
   SM_CHECK(hipMemcpyAsync(ctx->in.p, compressed, n, hipMemcpyHostToDevice, s));
+  HT("uncompress: H2D input")
   // a large stream: fragments in parallel when it is block-structured (Snappy.jl, libsnappy
   // and this library all write such streams); otherwise, or on any error, the in-order decode
   size_t hdr = 0;
   (void)sm_parse32((const uint8_t*)compressed, n, 0, &size, &hdr);
   if (size >= kParallelMinOutput && n - hdr >= 2 * sm::kIdxChunk) {
-    const int r = parallel_uncompress(ctx, (const uint8_t*)compressed, (uint32_t)n, (uint32_t)hdr, size);
+    bool copied = false;
+    const int r = parallel_uncompress(ctx, (const uint8_t*)compressed, (uint32_t)n, (uint32_t)hdr, size,
+                                      (uint8_t*)uncompressed, &copied);
     if (r < 0) return SM_ERR_DEVICE;
     if (r >= 1) {
       ctx->last_path = r;
-      SM_CHECK(hipMemcpyAsync(uncompressed, ctx->out.p, size, hipMemcpyDeviceToHost, s));
-      SM_CHECK(hipStreamSynchronize(s));
+      if (!copied) {
+        SM_CHECK(hipMemcpyAsync(uncompressed, ctx->out.p, size, hipMemcpyDeviceToHost, s));
+        SM_CHECK(hipStreamSynchronize(s));
+      }
+      HT("uncompress: D2H output")
       *uncompressed_length = size;
       return SM_OK;
     }

@@ -715,7 +715,7 @@ __device__ inline uint32_t window_tags(const uint8_t* buf, uint32_t rel0, uint32
 }
 
 __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
-                                                     uint32_t* rec_exit, uint32_t* rec_out) {
+                                                     uint2* rec) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kIdxChunk + kIdxPad];
   __shared__ __attribute__((aligned(16))) uint16_t jt[6 * 256];  // walk tables, then the entry walk's 3 KiB
   __shared__ uint32_t bm[kIdxChunk / 32];  // positions on lane 0's path
@@ -828,8 +828,8 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
     }
     __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the next window's stores follow these reads
   }
-  rec_exit[c * kIdxEntries + lane] = (uint32_t)min(ex, (uint64_t)0xffffffffu);
-  rec_out[c * kIdxEntries + lane] = res;
+  // (exit, output) pairs side by side: the host's walk over the records reads one cache line
+  rec[c * kIdxEntries + lane] = make_uint2((uint32_t)min(ex, (uint64_t)0xffffffffu), res);
 }
 
 __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
@@ -1106,10 +1106,10 @@ hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t s
   return hipGetLastError();
 }
 
-hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec_exit,
-                               uint32_t* rec_out, hipStream_t s) {
+hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec,
+                               hipStream_t s) {
   if (nchunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_stream_index, dim3(nchunks), dim3(64), 0, s, in, N, ip0, rec_exit, rec_out);
+  hipLaunchKernelGGL(k_stream_index, dim3(nchunks), dim3(64), 0, s, in, N, ip0, reinterpret_cast<uint2*>(rec));
   return hipGetLastError();
 }
 

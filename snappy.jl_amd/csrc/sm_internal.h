@@ -54,8 +54,9 @@ hipError_t launch_validate(const uint8_t* in, const uint64_t* in_off, const uint
                            int32_t* status, hipStream_t s);
 hipError_t launch_uncompressed_length(const uint8_t* in, const uint64_t* in_off, const uint32_t* in_len,
                                       uint32_t nblk, uint32_t* out_len, int32_t* status, hipStream_t s);
-hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec_exit,
-                               uint32_t* rec_out, hipStream_t s);
+// rec: nchunks * kIdxEntries (exit, output) u32 pairs
+hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec,
+                               hipStream_t s);
 hipError_t launch_decompress_frags(const uint8_t* in, uint32_t N, uint32_t size, uint8_t* out,
                                    const StreamFrag* frags, uint32_t nfrag, int32_t* status, hipStream_t s);
 // Any large stream (copies may reach into earlier blocks): origin pointers per output byte,
