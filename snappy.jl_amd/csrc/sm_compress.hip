@@ -291,18 +291,29 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         // bytes [0, 4) of a round are the verification (:238; known equal after a probe hit),
         // the rest find_match_length (:216).  Reads past the block return 0 and are capped.
         const uint32_t avail = n - ip;
-        uint32_t f, A, rb = 0;
-        for (;;) {
-          const uint32_t off = rb + 4 * lane;
-          A = S.word(ip + off);
-          const uint32_t x = A ^ S.word(cand + off);
-          const uint32_t fb = x ? (uint32_t)(__builtin_ctz(x) >> 3) : 4u;
-          const uint64_t m = ballot(fb < 4 || off + 4 >= avail);
-          if (m) {
-            f = min(readlane(off + fb, ctz64(m)), avail);
-            break;
+        // first mismatching byte of a lane's word, 4 if none (ffbl(0) = ~0)
+        auto fbyte = [](uint32_t x) {
+          uint32_t r;
+          asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+          return min(r >> 3, 4u);
+        };
+        uint32_t A = S.word(ip + 4 * lane);
+        uint32_t fb = fbyte(A ^ S.word(cand + 4 * lane));
+        uint64_t m = ballot(fb < 4 || 4 * lane + 4 >= avail);
+        uint32_t f, rb = 0;
+        if (m) {
+          f = min(readlane(4 * lane + fb, ctz64(m)), avail);
+        } else {
+          for (;;) {  // matches of 256 bytes and more
+            rb += 4 * kWave;
+            const uint32_t off = rb + 4 * lane;
+            fb = fbyte(S.word(ip + off) ^ S.word(cand + off));
+            m = ballot(fb < 4 || off + 4 >= avail);
+            if (m) {
+              f = min(readlane(off + fb, ctz64(m)), avail);
+              break;
+            }
           }
-          rb += 4 * kWave;
         }
         STAMP(2)
         if (f < 4) break;                                                      // :238
