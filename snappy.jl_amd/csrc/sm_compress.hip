@@ -58,8 +58,8 @@ __device__ inline uint32_t put_copy(uint8_t* dst, uint32_t op, uint32_t offset, 
 //
 //  * Five parses per CU.  The block is read in place from HBM through a buffer resource
 //    (range-checked to exactly the block; its lines stay in L2), and the
-//    only LDS is the 32 KiB table of 16 K u16 entries in the reference's own encoding,
-//    (pos - 1) mod 2^16 with 0xffff = empty = candidate 0 (Snappy.jl:30, internal.jl:190-191).
+//    only LDS is the 32 KiB table of 16 K u16 positions (0 = empty = candidate 0, as the
+//    reference's 0xffff fill reads, Snappy.jl:30, internal.jl:190-191).
 //    Staging the block in LDS instead fits one parse per CU (1.1-2.8 GB/s measured).
 //  * Batched exact probes.  After every copy the literal search probes positions p0 + D[k],
 //    D[0] = 0, D[k+1] = D[k] + (skip_k >> 5), skip_0 = 32, skip_{k+1} = skip_k + (skip_k >> 5)
@@ -100,13 +100,16 @@ struct BlockBytes {
   __device__ uint32_t byte(uint32_t pos) const { return __builtin_amdgcn_raw_buffer_load_b8(r, (int)pos, 0, 0); }
 };
 
-// Table entry h is half (h & 1) of dword h >> 1.  The probe's exchange and its wait are one asm
-// statement with an early-clobber result, so the compiler cannot copy the result register
-// before the data lands.  Returns the entry's old value.
+// Table entry h is half (h & 1) of dword h >> 1 and holds a position, 0 when never written.
+// The reference stores pos - 1 with 0xffff = empty and reads candidate (entry + 1) mod 2^16
+// (Snappy.jl:30, internal.jl:190-191): the same candidates, position 0 and "empty" alike
+// giving 0, without the decode on the parse's chain.  The probe's exchange and its wait are
+// one asm statement with an early-clobber result, so the compiler cannot copy the result
+// register before the data lands.  Returns the entry's old value (the candidate).
 __device__ inline uint32_t tab_probe(uint32_t* t, uint32_t h, uint32_t p) {
   const uint32_t sh = (h & 1u) << 4;
   const uint32_t addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint32_t*)(&t[h >> 1]));
-  const uint32_t mk = 0xffffu << sh, v = ((p - 1) & 0xffffu) << sh;
+  const uint32_t mk = 0xffffu << sh, v = p << sh;
   uint32_t old;
   asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)"
                : "=&v"(old)
@@ -114,7 +117,6 @@ __device__ inline uint32_t tab_probe(uint32_t* t, uint32_t h, uint32_t p) {
                : "memory");
   return (old >> sh) & 0xffffu;
 }
-__device__ inline uint32_t tab_cand(uint32_t raw) { return (raw + 1) & 0xffffu; }  // :190
 
 // wave-cooperative copy of len block bytes from s to global memory (16-byte stores in the body)
 __device__ inline void copy_to_global(const BlockBytes& S, uint8_t* __restrict__ g, uint32_t s, uint32_t len,
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
   S.nm4 = n - 4;
   const uint32_t tsize = a.table_size ? a.table_size : hashtable_size(n);      // Snappy.jl:27 (Q2)
   const uint32_t shift = 32 - (31 - __builtin_clz(tsize));                     // internal.jl:128
-  for (uint32_t k = lane; k < tsize / 2; k += kWave) stab[k] = 0xffffffffu;    // Snappy.jl:30
+  for (uint32_t k = lane; k < tsize / 2; k += kWave) stab[k] = 0;              // Snappy.jl:30
   // probe offsets D[64 i + lane] and D[64 i + lane + 1] (:170-172), in registers
   uint32_t Dk[kProbeSteps] = {}, Dn[kProbeSteps] = {};
   {
@@ -270,7 +272,7 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         const uint32_t h = hash32(cur, shift);
         uint32_t raw = 0;
         if (valid) raw = tab_probe(stab, h, p);
-        const uint32_t c = tab_cand(raw);
+        const uint32_t c = raw;                                                // :190
         const bool hit = valid && S.word(c) == cur;                            // :193
         const uint64_t hm = ballot(hit);
         if (hm) {
@@ -299,7 +301,9 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         };
         uint32_t A = S.word(ip + 4 * lane);
         uint32_t fb = fbyte(A ^ S.word(cand + 4 * lane));
-        uint64_t m = ballot(fb < 4 || 4 * lane + 4 >= avail);
+        // lanes whose word reaches the end (4 lane + 4 >= avail) stop the round too
+        const uint64_t lim0 = avail > 4 * kWave ? 0ull : ~0ull << ((avail - 1) >> 2);
+        uint64_t m = ballot(fb < 4) | lim0;
         uint32_t f, rb = 0;
         if (m) {
           f = min(readlane(4 * lane + fb, ctz64(m)), avail);
@@ -346,12 +350,12 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         uint32_t raw = 0;
         if (lane == 0) {
           uint16_t* u = reinterpret_cast<uint16_t*>(stab);
-          u[hash32(wp, shift)] = (uint16_t)(ip - 2);
+          u[hash32(wp, shift)] = (uint16_t)(ip - 1);
           const uint32_t h2 = hash32(wc, shift);
           raw = u[h2];
-          u[h2] = (uint16_t)(ip - 1);
+          u[h2] = (uint16_t)ip;
         }
-        cand = tab_cand(readlane(raw, 0));
+        cand = readlane(raw, 0);
         STAMP(3)
       }
     }
