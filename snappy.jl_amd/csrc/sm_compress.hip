@@ -322,18 +322,32 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         STAMP(2)
         if (f < 4) break;                                                      // :238
         STAMP_COUNT(6, 1)
-        tk = writelane(ip | ((ip - cand) << 16), ntok, tk);
-        tl = writelane(f, ntok, tl);
-        ++ntok;
-        const bool inreg = rb == 0 && f <= 4 * kWave - 4;
-        uint32_t wp = 0, wc = 0;
-        if (inreg) {  // the words at ip+f-1 and ip+f, from lanes (f-1)/4 and (f-1)/4 + 1
+        // The next candidate first (:228-235, one lane: insert ip-1, read and replace the entry
+        // for ip), so the bookkeeping below runs under its LDS round trip.  Past ip_limit the
+        // inserts are never read: the parse ends there.
+        const uint32_t ipn = ip + f;                                           // :217-220
+        uint32_t wp, wc;
+        if (rb == 0 && f <= 4 * kWave - 4) {  // the words at ipn-1 and ipn, from lanes (f-1)/4, +1
           const uint32_t k = (f - 1) >> 2, r8 = ((f - 1) & 3u) << 3;
           const uint64_t w = ((uint64_t)readlane(A, k + 1) << 32) | readlane(A, k);
           wp = (uint32_t)(w >> r8);
           wc = (uint32_t)(w >> (r8 + 8));
+        } else {
+          wp = uniform(S.word(ipn - 1));
+          wc = uniform(S.word(ipn));
         }
-        ip += f;                                                               // :217-220
+        uint32_t raw = 0;
+        if (lane == 0) {
+          uint16_t* u = reinterpret_cast<uint16_t*>(stab);
+          u[hash32(wp, shift)] = (uint16_t)(ipn - 1);
+          const uint32_t h2 = hash32(wc, shift);
+          raw = u[h2];
+          u[h2] = (uint16_t)ipn;
+        }
+        tk = writelane(ip | ((ip - cand) << 16), ntok, tk);
+        tl = writelane(f, ntok, tl);
+        ++ntok;
+        ip = ipn;
         next_emit = ip;
         if (ntok == kWave) {
           STAMP(3)
@@ -342,19 +356,6 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
           STAMP(1)
         }
         if ((int32_t)ip >= ip_limit) goto emit_remainder;                      // :222
-        if (!inreg) {
-          wp = uniform(S.word(ip - 1));
-          wc = uniform(S.word(ip));
-        }
-        // :228-235, one lane: insert ip-1, then read and replace the entry for ip
-        uint32_t raw = 0;
-        if (lane == 0) {
-          uint16_t* u = reinterpret_cast<uint16_t*>(stab);
-          u[hash32(wp, shift)] = (uint16_t)(ip - 1);
-          const uint32_t h2 = hash32(wc, shift);
-          raw = u[h2];
-          u[h2] = (uint16_t)ip;
-        }
         cand = readlane(raw, 0);
         STAMP(3)
       }
