@@ -13,10 +13,10 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/
   python3 bench.py --no-cpu > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench trace failed"; tail -5 "$OUT/bench.err"; exit 1; }
 # per-workload kernel traces (one op, one workload per run, so each kernel's average is that
 # workload's launch duration -- the bench trace above mixes text, random and config-5 launches)
-for W in "compress_fast text" "uncompress text" "compress_fast random" "uncompress random"; do
+for W in "compress_fast text" "uncompress text" "compress_fast random" "uncompress random" "compress_ref text" "compress_ref random"; do
   set -- $W
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$1_$2" -o k -- \
-    python3 tools/kbench.py --op $1 --data $2 --blocks 10000 --reps 20 > "$OUT/kb_$1_$2.log" 2>&1 || { echo "trace $W failed"; exit 1; }
+    python3 tools/kbench.py --op $1 --data $2 --blocks 10000 --reps ${REPS:-20} > "$OUT/kb_$1_$2.log" 2>&1 || { echo "trace $W failed"; exit 1; }
 done
 export BLOCKS=10000
 bash tools/pmc_run.sh compress_fast "$OUT/pmc_compress" text || exit 1
