@@ -772,8 +772,8 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   SM_CHECK(hipMemcpyAsync(d_in_len, in_len.data(), 4 * (size_t)nfrag, hipMemcpyHostToDevice, s));
   // Large inputs go up in pieces on the copy stream, and each piece's fragments compress as
   // soon as it lands, so the kernels run under the rest of the upload.
-  const uint32_t npiece = n >= kPipeMinInput ? (nfrag + kPieceFrags - 1) / kPieceFrags : 1;
-  if (npiece > 1) SM_CHECK(ensure_copy_stream(ctx, npiece));
+  uint32_t npiece = n >= kPipeMinInput ? (nfrag + kPieceFrags - 1) / kPieceFrags : 1;
+  if (npiece > 1 && ensure_copy_stream(ctx, npiece) != hipSuccess) npiece = 1;  // one upload then
   for (uint32_t pc = 0; pc < npiece; ++pc) {
     const uint32_t f0 = pc * kPieceFrags, f1 = npiece == 1 ? nfrag : std::min(nfrag, f0 + kPieceFrags);
     const size_t b0 = (size_t)f0 * SM_BLOCK_SIZE, b1 = std::min(n, (size_t)f1 * SM_BLOCK_SIZE);
