@@ -127,14 +127,19 @@ __device__ inline void copy_to_global(const BlockBytes& S, uint8_t* __restrict__
   g += head; s += head; len -= head;
   const uint32_t n16 = len >> 4;
   uint4* g16 = reinterpret_cast<uint4*>(g);
-  for (uint32_t k = lane; k < n16; k += kWave) {
-    const uint32_t p = s + 16 * k;
-    uint4 v;
-    v.x = S.word(p);
-    v.y = S.word(p + 4);
-    v.z = S.word(p + 8);
-    v.w = S.word(p + 12);
-    g16[k] = v;
+  // four 16-byte units per lane per step, all loads issued before the stores (a whole
+  // incompressible block is one literal: 64 steps of one load round trip each otherwise)
+  constexpr uint32_t kU = 4;
+  for (uint32_t k0 = lane; k0 < n16; k0 += kU * kWave) {
+    uint4 v[kU];
+#pragma unroll
+    for (uint32_t i = 0; i < kU; ++i) {
+      const uint32_t p = s + 16 * (k0 + i * kWave);
+      if (k0 + i * kWave < n16) v[i] = make_uint4(S.word(p), S.word(p + 4), S.word(p + 8), S.word(p + 12));
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kU; ++i)
+      if (k0 + i * kWave < n16) g16[k0 + i * kWave] = v[i];
   }
   const uint32_t done = n16 << 4;
   if (lane < len - done) g[done + lane] = (uint8_t)S.byte(s + done + lane);
