@@ -57,10 +57,10 @@ __device__ inline uint32_t put_copy(uint8_t* dst, uint32_t op, uint32_t offset, 
 // times how short each parse's dependency chain is:
 //
 //  * Five parses per CU.  The block is read in place from HBM through a buffer resource
-//    (range-checked to exactly the block; its lines stay in L2), and the
-//    only LDS is the 32 KiB table of 16 K u16 positions (0 = empty = candidate 0, as the
-//    reference's 0xffff fill reads, Snappy.jl:30, internal.jl:190-191).
-//    Staging the block in LDS instead fits one parse per CU (1.1-2.8 GB/s measured).
+//    (range-checked to exactly the block; its lines stay in L2), and the only LDS is the
+//    32 KiB table of 16 K u16 positions (0 = empty = candidate 0, as the reference's 0xffff
+//    fill reads, Snappy.jl:30, internal.jl:190-191).
+//    Staging the block in LDS instead fits one parse per CU (2.3-2.8 GB/s measured).
 //  * Batched exact probes.  After every copy the literal search probes positions p0 + D[k],
 //    D[0] = 0, D[k+1] = D[k] + (skip_k >> 5), skip_0 = 32, skip_{k+1} = skip_k + (skip_k >> 5)
 //    (:162-175): a fixed sequence, so 64 probes go in one step, lane j = probe k0 + j.  Probe k
@@ -86,8 +86,8 @@ constexpr uint32_t kProbeSteps = kMaxProbes / kWave;
 constexpr uint32_t kTabBytes = 2 * kMaxHashTableSize;
 
 // The block in HBM through a raw buffer resource over exactly [0, n): a dword load at offset o
-// returns 0 when o + 4 > n (the whole dword; measured on gfx950, tools/probes/buffer_range.hip), and unaligned
-// dword loads are served.  word(pos) therefore loads at min(pos, n - 4) and shifts, so the
+// returns 0 when o + 4 > n (the whole dword), and unaligned dword loads are served (both
+// measured on gfx950, tools/probes/buffer_range.hip).  word(pos) therefore loads at min(pos, n - 4) and shifts, so the
 // bytes below n are exact and the bytes past it read 0 (the zero slack the reference's
 // find_match_length never compares) -- and no load touches memory past the block.
 struct BlockBytes {
