@@ -87,9 +87,10 @@ constexpr uint32_t kTabBytes = 2 * kMaxHashTableSize;
 
 // The block in HBM through a raw buffer resource over exactly [0, n): a dword load at offset o
 // returns 0 when o + 4 > n (the whole dword), and unaligned dword loads are served (both
-// measured on gfx950, tools/probes/buffer_range.hip).  word(pos) therefore loads at min(pos, n - 4) and shifts, so the
-// bytes below n are exact and the bytes past it read 0 (the zero slack the reference's
-// find_match_length never compares) -- and no load touches memory past the block.
+// measured on gfx950, tools/probes/buffer_range.hip).  word(pos) therefore loads at
+// min(pos, n - 4) and shifts, so the bytes below n are exact and the bytes past it read 0
+// (the zero slack the reference's find_match_length never compares) -- and no load touches
+// memory past the block.
 struct BlockBytes {
   __amdgpu_buffer_rsrc_t r;
   uint32_t nm4;  // n - 4 (word() is used only when n >= 15)
