@@ -342,14 +342,12 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
           wp = uniform(S.word(ipn - 1));
           wc = uniform(S.word(ipn));
         }
-        uint32_t raw = 0;
-        if (lane == 0) {
-          uint16_t* u = reinterpret_cast<uint16_t*>(stab);
-          u[hash32(wp, shift)] = (uint16_t)(ipn - 1);
-          const uint32_t h2 = hash32(wc, shift);
-          raw = u[h2];
-          u[h2] = (uint16_t)ipn;
-        }
+        // (every lane stores the same value at the same address: one lane's store, no exec mask)
+        uint16_t* u = reinterpret_cast<uint16_t*>(stab);
+        u[hash32(wp, shift)] = (uint16_t)(ipn - 1);
+        const uint32_t h2 = hash32(wc, shift);
+        const uint32_t raw = u[h2];
+        u[h2] = (uint16_t)ipn;
         tk = writelane(ip | ((ip - cand) << 16), ntok, tk);
         tl = writelane(f, ntok, tl);
         ++ntok;
