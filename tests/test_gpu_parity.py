@@ -530,3 +530,20 @@ def test_uncompress_origin_path_cases(sm, oracle, gpu_available):
         assert sm.uncompress(s) == e
         assert sm.last_uncompress_path() == 2
         assert sm.validate(s) == 0
+
+
+def test_host_path_piece_boundaries(sm, oracle, gpu_available):
+    """The single-buffer host path's pipelining (sm_api.hip): inputs from 32 MiB upload in
+    16 MiB pieces with per-piece compress kernels, outputs over 128 MiB download in pieces under
+    the fragment decode.  Sizes just past each threshold, with partial last pieces."""
+    base = _big_corpus(8 << 20)
+    for n in ((32 << 20) + 12345, (128 << 20) + 7):
+        raw = (base * (n // len(base) + 1))[:n]
+        fast = sm.compress(raw, mode="fast")
+        assert oracle.uncompress(fast) == raw
+        assert sm.uncompress(fast) == raw
+        assert sm.last_uncompress_path() == 1
+        if n < (64 << 20):
+            ref = sm.compress(raw, mode="reference")
+            assert ref == oracle.compress(raw)
+            assert sm.uncompress(ref) == raw
