@@ -1,3 +1,8 @@
+// Buffer-resource probe (design tool, GPU box): what a raw buffer dword load returns at and past
+// num_records (6 here), from an aligned and from a misaligned base.  Measured on gfx950: a load
+// at offset o returns 0 when o + 4 > num_records (the whole dword), and unaligned loads are
+// served -- the basis of the reference-mode compressor's exact block bounds (sm_compress.hip).
+//   hipcc --offload-arch=gfx950 -O2 -o /tmp/buffer_range tools/probes/buffer_range.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
