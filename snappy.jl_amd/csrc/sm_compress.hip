@@ -294,7 +294,7 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         if (ballot(valid) != ~0ull) break;                                     // :175 -> remainder
       }
       STAMP(0)
-      if (!found) goto emit_remainder;
+      if (!found) break;                                                       // -> remainder
       for (;;) {                                                               // :211-239
         // bytes [0, 4) of a round are the verification (:238; known equal after a probe hit),
         // the rest find_match_length (:216).  Reads past the block return 0 and are capped.
@@ -359,13 +359,13 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
           ntok = 0;
           STAMP(1)
         }
-        if ((int32_t)ip >= ip_limit) goto emit_remainder;                      // :222
+        if ((int32_t)ip >= ip_limit) break;                                    // :222
         cand = readlane(raw, 0);
         STAMP(3)
       }
+      if ((int32_t)ip >= ip_limit) break;                                      // :222 -> remainder
     }
   }
-emit_remainder:
   if (ntok) op = flush_copies(S, dst, op, base, ntok, tk, tl, lane);
   if (next_emit <= e) op = emit_literal_w(S, dst, op, next_emit, e - next_emit + 1, lane);  // :244-248
   STAMP(5)
