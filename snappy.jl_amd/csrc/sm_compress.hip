@@ -267,31 +267,31 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
       ip += 1;                                                                 // :163
       // literal search, 64 probes per step (:167-194)
       const uint32_t p0 = ip;
-      uint32_t cand = 0;
-      bool found = false;
+      // the step that ends the search: its lanes' position, hash, old entry and validity
+      uint32_t p = 0, h = 0, raw = 0;
+      bool valid = false;
+      uint64_t hm = 0;
 #pragma unroll
       for (uint32_t i = 0; i < kProbeSteps; ++i) {
         STAMP_COUNT(7, 1)
-        const uint32_t p = p0 + Dk[i];
-        const bool valid = (int32_t)(p0 + Dn[i]) <= ip_limit;                 // :175
+        p = p0 + Dk[i];
+        valid = (int32_t)(p0 + Dn[i]) <= ip_limit;                             // :175
         const uint32_t cur = S.word(p);
-        const uint32_t h = hash32(cur, shift);
-        uint32_t raw = 0;
-        if (valid) raw = tab_probe(stab, h, p);
-        const uint32_t c = raw;                                                // :190
-        const bool hit = valid && S.word(c) == cur;                            // :193
-        const uint64_t hm = ballot(hit);
-        if (hm) {
-          const uint32_t j = ctz64(hm);
-          const uint32_t pj = readlane(p, j);
-          if (valid && lane > j && c <= pj)                                    // undo later probes
-            reinterpret_cast<uint16_t*>(stab)[h] = (uint16_t)raw;
-          ip = pj;
-          cand = readlane(c, j);
-          found = true;
-          break;
-        }
-        if (ballot(valid) != ~0ull) break;                                     // :175 -> remainder
+        h = hash32(cur, shift);
+        raw = 0;
+        if (valid) raw = tab_probe(stab, h, p);                                // :190 (raw = candidate)
+        hm = ballot(valid && S.word(raw) == cur);                              // :193
+        if (hm || ballot(valid) != ~0ull) break;                               // a match, or :175
+      }
+      const bool found = hm != 0;
+      uint32_t cand = 0;
+      if (found) {
+        const uint32_t j = ctz64(hm);
+        const uint32_t pj = readlane(p, j);
+        if (valid && lane > j && raw <= pj)                                    // undo later probes
+          reinterpret_cast<uint16_t*>(stab)[h] = (uint16_t)raw;
+        ip = pj;
+        cand = readlane(raw, j);
       }
       STAMP(0)
       if (!found) break;                                                       // -> remainder
