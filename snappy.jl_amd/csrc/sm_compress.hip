@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
       }
       const bool found = hm != 0;
       uint32_t cand = 0;
-      if (found) {
+      if (__builtin_expect(found, 1)) {
         const uint32_t j = ctz64(hm);
         const uint32_t pj = readlane(p, j);
         if (valid && lane > j && raw <= pj)                                    // undo later probes
@@ -294,7 +294,7 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         cand = readlane(raw, j);
       }
       STAMP(0)
-      if (!found) break;                                                       // -> remainder
+      if (__builtin_expect(!found, 0)) break;                                  // -> remainder
       for (;;) {                                                               // :211-239
         // bytes [0, 4) of a round are the verification (:238; known equal after a probe hit),
         // the rest find_match_length (:216).  Reads past the block return 0 and are capped.
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         const uint64_t lim0 = avail > 4 * kWave ? 0ull : ~0ull << ((avail - 1) >> 2);
         uint64_t m = ballot(fb < 4) | lim0;
         uint32_t f, rb = 0;
-        if (m) {
+        if (__builtin_expect(m != 0, 1)) {
           f = min(readlane(4 * lane + fb, ctz64(m)), avail);
         } else {
           for (;;) {  // matches of 256 bytes and more
@@ -326,14 +326,14 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
           }
         }
         STAMP(2)
-        if (f < 4) break;                                                      // :238
+        if (__builtin_expect(f < 4, 0)) break;                                 // :238
         STAMP_COUNT(6, 1)
         // The next candidate first (:228-235, one lane: insert ip-1, read and replace the entry
         // for ip), so the bookkeeping below runs under its LDS round trip.  Past ip_limit the
         // inserts are never read: the parse ends there.
         const uint32_t ipn = ip + f;                                           // :217-220
         uint32_t wp, wc;
-        if (rb == 0 && f <= 4 * kWave - 4) {  // the words at ipn-1 and ipn, from lanes (f-1)/4, +1
+        if (__builtin_expect(rb == 0 && f <= 4 * kWave - 4, 1)) {  // words at ipn-1, ipn: lanes (f-1)/4, +1
           const uint32_t k = (f - 1) >> 2, r8 = ((f - 1) & 3u) << 3;
           const uint64_t w = ((uint64_t)readlane(A, k + 1) << 32) | readlane(A, k);
           wp = (uint32_t)(w >> r8);
@@ -353,17 +353,17 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         ++ntok;
         ip = ipn;
         next_emit = ip;
-        if (ntok == kWave) {
+        if (__builtin_expect(ntok == kWave, 0)) {
           STAMP(3)
           op = flush_copies(S, dst, op, base, ntok, tk, tl, lane);
           ntok = 0;
           STAMP(1)
         }
-        if ((int32_t)ip >= ip_limit) break;                                    // :222
+        if (__builtin_expect((int32_t)ip >= ip_limit, 0)) break;               // :222
         cand = readlane(raw, 0);
         STAMP(3)
       }
-      if ((int32_t)ip >= ip_limit) break;                                      // :222 -> remainder
+      if (__builtin_expect((int32_t)ip >= ip_limit, 0)) break;                 // :222 -> remainder
     }
   }
   if (ntok) op = flush_copies(S, dst, op, base, ntok, tk, tl, lane);
