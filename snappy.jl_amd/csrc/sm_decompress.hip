@@ -289,7 +289,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   while ((int64_t)ip < Nm1 && op < op_lim) {
     STAMP_COUNT(6, 1)
     if (ip >= wb + 256) {
-      if (ip < wb + 512) {
+      if (__builtin_expect(ip < wb + 512, 1)) {
         ring_put(ring, wb + 768, pre1, lane);
         pre1 = pre2;
         wb += 256;
@@ -308,7 +308,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     const uint32_t ntok = walk_window(ring_get8(ring, ip + 4 * lane), wlim - ip, jt, lane, cpos, csz, sizes);
     uint32_t tpos = 0, ipw = ip, tnext = 0;
     bool big = false;
-    if (ntok) {
+    if (__builtin_expect(ntok != 0, 1)) {
       tpos = ip + cpos;
       tnext = cpos + csz;
       ipw = ip + readlane(tnext, ntok - 1);
@@ -319,7 +319,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     }
 
     STAMP(1)
-    if (ntok) {
+    if (__builtin_expect(ntok != 0, 1)) {
       const bool mine = lane < ntok;
       const uint64_t hv = ring_get8(ring, mine ? tpos : wb);
       const uint32_t c = (uint32_t)hv & 0xff;
@@ -349,11 +349,11 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         err = !mine ? kOk : (iscopy ? ec : (e_lit ? kErrLiteral : kOk));
       }
       const uint64_t em = ballot(err != kOk);
-      if (em) return (int32_t)readlane((uint32_t)err, ctz64(em));
+      if (__builtin_expect(em != 0, 0)) return (int32_t)readlane((uint32_t)err, ctz64(em));
       // cap the batch output at kBatchOut bytes (the window bound; one tag is <= 200 B) and at
       // the output limit (a fragment ends where the next one starts)
       uint32_t nt = ntok;
-      if (readlane(incl, ntok - 1) > kBatchOut || readlane(opt, ntok - 1) >= op_lim) {
+      if (__builtin_expect(readlane(incl, ntok - 1) > kBatchOut || readlane(opt, ntok - 1) >= op_lim, 0)) {
         nt = (uint32_t)__builtin_popcountll(ballot(mine && incl <= kBatchOut && opt < op_lim));
         ipw = ip + readlane(tnext, nt - 1);
         big = false;  // the next tag is a batch tag inside the window
@@ -394,7 +394,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       //    chunk i = S from phase m = 8i mod offset, wrapping once to S's start (offset >= 8);
       //    for offset < 8 the period is unrolled to 16 bytes in registers.
       if (SM_ABLATE_D & 1) done = ~0ull;
-      if (done != ~0ull) {
+      if (__builtin_expect(done != ~0ull, 1)) {
         STAMP_COUNT(7, 1)
         const bool ready = !((done >> lane) & 1) && ((SM_ABLATE_D & 2) || !iscopy || shi <= O0);
         const uint64_t rm = ballot(ready);
@@ -465,7 +465,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
             }
           }
         };
-        if (gtail) rounds(std::true_type{});
+        if (__builtin_expect(gtail, 0)) rounds(std::true_type{});
         else rounds(std::false_type{});
         done |= rm;
       }
@@ -493,7 +493,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
       STAMP(4)
       op += X;
-      if (op > op_lim) return kErrCross;  // a tag crosses the fragment end
+      if (__builtin_expect(op > op_lim, 0)) return kErrCross;  // a tag crosses the fragment end
       win_flush(out, win, flushed, op & ~15u, lane);  // whole 16-byte blocks to HBM
       flushed = max(flushed, op & ~15u);
       ip = ipw;
@@ -503,7 +503,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       issue_pre2 = false;
     }
 
-    if (big && op < op_lim) {  // (at op_lim the literal opens the next fragment)
+    if (__builtin_expect(big && op < op_lim, 0)) {  // (at op_lim the literal opens the next fragment)
       // one literal too long for the batch path (or a wrapped length): straight to HBM
       const uint64_t hv = ring_get8(ring, ip);
       const uint32_t c = uniform((uint32_t)hv & 0xff);
