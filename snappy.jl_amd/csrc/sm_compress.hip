@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         const uint32_t cur = S.word(p);
         h = hash32(cur, shift);
         raw = 0;
-        if (valid) raw = tab_probe(stab, h, p);                                // :190 (raw = candidate)
+        if (__builtin_expect(valid, 1)) raw = tab_probe(stab, h, p);                                // :190 (raw = candidate)
         hm = ballot(valid && S.word(raw) == cur);                              // :193
         if (hm || ballot(valid) != ~0ull) break;                               // a match, or :175
       }
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
             const uint32_t off = rb + 4 * lane;
             fb = fbyte(S.word(ip + off) ^ S.word(cand + off));
             m = ballot(fb < 4 || off + 4 >= avail);
-            if (m) {
+            if (__builtin_expect(m != 0, 1)) {
               f = min(readlane(off + fb, ctz64(m)), avail);
               break;
             }
