@@ -177,6 +177,9 @@ __device__ inline uint32_t fast_hash(uint32_t w) {
 // which leave LDS for one chunk per wave (15 chunks, 3840 positions).  Both rings are 30 KiB.
 template <int D>
 struct Cfg {
+#ifndef SM_FAST_LASTINS  // 1: the inserter parses the final round's chunk slot kPW (see the round loop)
+#define SM_FAST_LASTINS 1
+#endif
 #ifndef SM_FAST_CPW
 #define SM_FAST_CPW 2
 #endif
@@ -601,7 +604,7 @@ __device__ inline RoundLayout round_layout(const uint32_t* cinfo, uint32_t r, ui
 
 template <int D>
 constexpr size_t fast_lds() {
-  return kBlockSize + kTabBytes + Cfg<D>::kRingBytes + 4 * 64 + kPW * kLevels * kRow + kPW * 8 * kP;
+  return kBlockSize + kTabBytes + Cfg<D>::kRingBytes + 4 * 64 + kWavesPerBlock * kLevels * kRow + kWavesPerBlock * 8 * kP;
 }
 static_assert(fast_lds<1>() <= 160 * 1024 && fast_lds<2>() <= 160 * 1024, "fast compressor LDS exceeds a CU");
 
@@ -623,9 +626,10 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
   const uint32_t wave = uniform(tid >> 6);
   const uint32_t lane = tid & 63;
   const bool inserter = wave == kPW;
-  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + 64) + (inserter ? 0 : wave) * kLevels * kRow;
-  uint64_t* tsw = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(csize + 64) + kPW * kLevels * kRow) +
-                  (inserter ? 0 : wave) * kP;  // per-wave copy-start bitmask
+  // per-wave jump tables and copy-start bitmasks (the inserter's are used in the final round)
+  uint8_t* jt = reinterpret_cast<uint8_t*>(csize + 64) + wave * kLevels * kRow;
+  uint64_t* tsw = reinterpret_cast<uint64_t*>(reinterpret_cast<uint8_t*>(csize + 64) + kWavesPerBlock * kLevels * kRow) +
+                  wave * kP;
 
   const uint32_t b = blockIdx.x;
   if (a.screened && a.out_len[b] != kScreenTodo) return;  // emitted as one literal by k_literal_screen
@@ -661,8 +665,8 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     uint4* t16 = reinterpret_cast<uint4*>(T);
     for (uint32_t k = tid; k < kTabBytes / 16; k += kThreads) t16[k] = z;  // 0 = no position
   }
-  if (!inserter && kEnd == kChunk && lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
-  if (!inserter && lane == 0) jt[kChunk] = (uint8_t)kEnd;  // NM past the chunk: no match
+  if (kEnd == kChunk && lane < kLevels) jt[lane * kRow + kChunk] = (uint8_t)kChunk;
+  if (lane == 0) jt[kChunk] = (uint8_t)kEnd;  // NM past the chunk: no match
   uint32_t op = 0;
   if (a.header) {
     uint32_t nb = varint_len(n);
@@ -689,7 +693,14 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
 #endif
     uint32_t* cinfo = csize + (r & 1) * 32;
     ChunkTok tk[C::kCPW];
-    if (inserter) {
+    // The final round has nothing left to insert.  A full 64 KiB block's final round holds 16
+    // chunks (256 = 8 x 30 + 16), so without help parse wave 0 takes slots 0 and 15 and the
+    // round lasts as long as a full one; the idle inserter parses slot kPW instead, and the
+    // round takes one chunk's time.  Wave 0 hands it the output offset (csize[63] is spare:
+    // chunk infos use csize[0..kSlots) of each half) before the round's barrier.
+    const bool ins_parse = SM_FAST_LASTINS && kSlots > kPW && r + 1 == rounds;
+    if (ins_parse && wave == 0 && lane == 0) csize[63] = op;
+    if (inserter && !ins_parse) {
       insert_round<kDepth>(T, ring + ((r + 1) & 1) * kRP, (r + 1) * kRP, n, lane);
       STAMP(8)
       STAMP_COUNT(10, 1)
@@ -697,12 +708,15 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       // parse wave w owns the round's chunk slots w, w + 15, ...
 #pragma unroll
       for (int u = 0; u < C::kCPW; ++u) {
-        const uint32_t slot = wave + kPW * u;
+        const uint32_t slot = inserter ? kPW : wave + kPW * u;
+        const bool mine = inserter ? u == 0 : !(ins_parse && slot == kPW);
         const uint32_t k = r * kSlots + slot;
         const uint32_t c0 = k * kChunk;
-        if (SM_FAST_PPRIO && u == 0) __builtin_amdgcn_s_setprio(1);
-        if (SM_FAST_PPRIO && u == 1) __builtin_amdgcn_s_setprio(0);
-        if (k < nchunks && (SM_ABLATE & 4)) {  // diagnostic: hashes only (the inserter needs them)
+        if (SM_FAST_PPRIO && u == 0 && !inserter) __builtin_amdgcn_s_setprio(1);
+        if (SM_FAST_PPRIO && u == 1 && !inserter) __builtin_amdgcn_s_setprio(0);
+        if (!mine) {
+          tk[u].c0 = tk[u].ce = c0;  // parsed (and its chunk info written) by the other wave
+        } else if (k < nchunks && (SM_ABLATE & 4)) {  // diagnostic: hashes only (the inserter needs them)
           Cand* cr = ring + (r & 1) * kRP + slot * kChunk;
           if (k + 2 * kSlots < nchunks) {
 #pragma unroll
@@ -732,10 +746,11 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
       STAMP(3)
     }
     __syncthreads();  // the round's chunk infos; the next round's candidates
-    if (inserter) {
+    if (inserter && !ins_parse) {
       STAMP(9)
       continue;
     }
+    if (inserter) op = csize[63];
     STAMP(4)
     if (SM_FAST_PPRIO) __builtin_amdgcn_s_setprio(2);
 
@@ -746,7 +761,7 @@ __global__ __launch_bounds__(kThreads) void k_compress_fast(CompressArgs a) {
     if (!(SM_ABLATE & 1)) {
 #pragma unroll
       for (int u = 0; u < C::kCPW; ++u) {
-        const uint32_t slot = wave + kPW * u;
+        const uint32_t slot = inserter ? kPW : wave + kPW * u;
         if (tk[u].ce > tk[u].c0)
           emit_chunk(dst, data, tk[u], op + readlane(inclm - Smv, slot), readlane(contv, slot), readlane(runv, slot), lane);
       }
