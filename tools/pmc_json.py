@@ -24,6 +24,7 @@ KERNELS = {"compress_fast": ("pmc_compress", ["k_literal_screen", "k_compress_fa
            "uncompress": ("pmc_uncompress", ["k_decompress("]),
            "compress_fast_random": ("pmc_compress_random", ["k_literal_screen", "k_compress_fast<1>"]),
            "uncompress_random": ("pmc_uncompress_random", ["k_decompress("])}
+IN_BYTES = 10000 * 65536  # uncompressed bytes per launch (tools/pmc_run.sh BLOCKS=10000)
 
 
 def main(root, out_path):
@@ -45,6 +46,9 @@ def main(root, out_path):
             "write_size_bytes": write,
             "hbm_bytes_per_launch": 2.0 * fetch + write,
             "counters": {k[:60]: {n: v for n, v in sorted(c.items())} for k, c in per.items()},
+            # issue-side figures per uncompressed input byte (10,000 x 64 KiB per launch)
+            "per_input_byte": {n: sum(c.get(n, 0.0) for c in per.values()) / IN_BYTES
+                               for n in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH")},
         }
     json.dump(res, open(out_path, "w"), indent=1)
     print(json.dumps({k: v.get("hbm_bytes_per_launch") for k, v in res.items() if isinstance(v, dict)}))
