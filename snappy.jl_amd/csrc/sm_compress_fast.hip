@@ -25,6 +25,8 @@
 //    write tag bytes, position lanes scatter literal bytes.
 // One barrier per round (chunk infos are double-buffered); the parse waves step their issue
 // priority down through a round so they cross it together.  Output is deterministic.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "sm_device.h"
@@ -950,6 +952,11 @@ hipError_t launch_compress_fast(const CompressArgs& a0, int mode, hipStream_t s)
   hipLaunchKernelGGL(k_literal_screen, dim3(a.nblk), dim3(kScrThreads), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  static const int old = [] {
+    const char* v = getenv("SM_FAST_OLD");
+    return v ? atoi(v) : 0;
+  }();
+  if (!old) return launch_compress_sc(a, s);
   return mode == 2 ? launch_depth<2>(a, s) : launch_depth<1>(a, s);
 }
 

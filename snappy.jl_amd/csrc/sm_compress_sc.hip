@@ -1,0 +1,612 @@
+// sm_compress_sc.hip -- fast-mode batched snappy compression for gfx950 (MI355X), round 3:
+// super-chunks with a token-passed insert, a wave-parallel verify and a LANE-SERIAL greedy walk.
+//
+// Output is a valid snappy stream per <= 64 KiB block: it decodes bit-exactly under Snappy.jl's
+// uncompress (src/internal.jl:411-466).  It is the reference's greedy parse (internal.jl:127-250)
+// with two changes that make it parallel: every position gets its candidates from an in-order
+// insert of ALL positions (not only the probed ones), and the block is cut into 1 KiB
+// super-chunks whose copies stop at the super-chunk end.
+//
+// One 16-wave workgroup per block; the block (64 KiB) and a 32 KiB hash table live in LDS.  Wave w
+// owns super-chunks w, w + 16, ... (64 positions per lane-group, 16 groups).  Per super-chunk:
+//  A. hash its 16 groups of 64 positions (the reference's multiply, internal.jl:94, 13 bits);
+//  B. wait for the insert token, then ONE ds_mskor_rtn_b32 per group exchanges the positions into
+//     the table and hands the token on.  A table dword holds two u16 slots (position + 1): group
+//     parity g & 1 picks the slot a position is written to, and the returned dword gives both
+//     candidates at once -- the latest earlier position of the same hash in the own slot (exact:
+//     a wave's LDS instructions execute in order, and the conflicting lanes of one instruction in
+//     ascending lane order) and the latest one of the other parity.  Correctness never depends on
+//     that order (every candidate is verified); only the ratio does;
+//  C. verify both candidates (8 bytes, then 16 where both fill 8), keep the longer, and store per
+//     position the match length (u8; 1/2 = "extend from 8/16") and offset (u16) in the wave's
+//     lane slices, plus the match bitmask;
+//  D. each LANE walks the 16 positions it owns greedily and serially (the reference's loop:
+//     literal runs are skipped through the bitmask, a match is extended 16 bytes a step up to 255
+//     bytes).  A copy can end inside a later lane's positions, so the walks are resynchronised:
+//     every lane starts at its first position, then lanes whose true start (the previous lane's
+//     end) differs walk again, until no start changes;
+//  E. literal runs that cross lanes get one tag (segmented scan), token sizes, a DPP scan;
+//  F. the super-chunk's output offset comes from the previous super-chunk (an LDS word), and
+//  G. each lane writes its tokens straight to global memory (16-byte stores whose tails the same
+//     lane overwrites later; exact stores at the lane's end).
+// Output is deterministic.
+#include "sm_device.h"
+#include "sm_internal.h"
+
+namespace sm {
+
+constexpr uint32_t kScreenTodoSc = 0xfffffffeu;  // k_literal_screen's "parse this block" mark
+
+constexpr uint32_t kScS = 1024;           // super-chunk bytes
+constexpr uint32_t kScC = kScS / 64;      // positions per lane (16)
+constexpr uint32_t kScG = kScS / 64;      // 64-position groups per super-chunk (16)
+constexpr uint32_t kScW = 16;             // waves per workgroup
+constexpr uint32_t kScThreads = 64 * kScW;
+constexpr uint32_t kScTabBits = 13;       // 8 K dwords = 16 K u16 slots
+constexpr uint32_t kScLP = kScC + 4;      // lane slice pitch of the length bytes (odd dword count: no bank conflicts)
+constexpr uint32_t kScOP = 2 * kScC + 4;  // lane slice pitch of the u16 offsets
+constexpr uint32_t kScMaxL = 255;         // longest copy token (u8 lengths)
+constexpr uint32_t kScMaxSc = kBlockSize / kScS;
+constexpr uint32_t kScSpinMax = 1u << 22;  // hand-off polls (64 cycles each) before a wait gives up
+static_assert(kScC == 16 && kScG == 16, "the walk keeps a lane's 16 positions in one u16 mask");
+
+#if SM_STAMP
+__device__ unsigned long long g_stamp_sc[12];
+#endif
+STAMP_MACROS(12)
+
+typedef uint4 __attribute__((aligned(1))) sc_u128u;
+typedef uint64_t __attribute__((aligned(1))) sc_u64u;
+typedef uint32_t __attribute__((aligned(1))) sc_u32u;
+typedef uint16_t __attribute__((aligned(1))) sc_u16u;
+
+struct ScLds {
+  uint8_t blk[kBlockSize + 64];             // the block (+ pad: reads run up to 20 bytes past a position)
+  uint32_t T[(1u << kScTabBits) + 4];       // hash table; T[1 << kScTabBits] is the dummy for invalid lanes
+  uint8_t L[kScW][64 * kScLP];              // per wave: match length byte of each position (lane slices)
+  uint8_t O[kScW][64 * kScOP];              // per wave: u16 offset of each position (lane slices)
+  uint64_t M[kScW][kScG];                   // per wave: match bitmask (bit = position of the super-chunk)
+  uint32_t ins;                             // insert token: super-chunks inserted so far
+  uint32_t err;                             // a hand-off wait timed out (never expected)
+  uint32_t base[kScMaxSc + 1];              // output offset of super-chunk k, + 1 (0: not known yet)
+};
+static_assert(sizeof(ScLds) <= 160 * 1024, "LDS");
+
+__device__ inline uint32_t sc_ld32(const uint8_t* blk, uint32_t a) { return *reinterpret_cast<const uint32_t*>(blk + a); }
+
+// 16 bytes of the block at p (five aligned dwords, four funnel shifts)
+__device__ inline uint4 sc_ld128(const uint8_t* blk, uint32_t p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(blk + (p & ~3u));
+  const uint32_t s = p & 3u;
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s),
+                    __builtin_amdgcn_alignbyte(w3, w2, s), __builtin_amdgcn_alignbyte(w4, w3, s));
+}
+
+// first differing byte of two 8-byte values given as dword pairs (8: equal)
+__device__ inline uint32_t sc_diff8(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
+  const uint32_t d0 = a0 ^ b0, d1 = a1 ^ b1;
+  return d0 ? (uint32_t)__builtin_ctz(d0) >> 3 : (d1 ? 4u + ((uint32_t)__builtin_ctz(d1) >> 3) : 8u);
+}
+
+// len (< 16 unless at + 16 <= oend) low bytes of v to dst[at..]: one 16-byte store when the lane's
+// output continues past it (the tail is garbage that this lane overwrites later), exact otherwise
+__device__ inline void sc_put(uint8_t* dst, uint32_t at, uint4 v, uint32_t len, uint32_t oend) {
+  if (at + 16 <= oend) {
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Walign-mismatch"
+    *reinterpret_cast<sc_u128u*>(dst + at) = v;  // unaligned global stores are served on gfx950
+#pragma clang diagnostic pop
+    return;
+  }
+  uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+  if (len & 8) {
+    *reinterpret_cast<sc_u64u*>(dst + at) = lo;
+    lo = hi;
+    at += 8;
+  }
+  if (len & 4) {
+    *reinterpret_cast<sc_u32u*>(dst + at) = (uint32_t)lo;
+    lo >>= 32;
+    at += 4;
+  }
+  if (len & 2) {
+    *reinterpret_cast<sc_u16u*>(dst + at) = (uint16_t)lo;
+    lo >>= 16;
+    at += 2;
+  }
+  if (len & 1) dst[at] = (uint8_t)lo;
+}
+
+// bytes v[0, len) (len 1..16) to the LDS byte array at byte address a (any alignment): up to five
+// masked ors (ds_mskor_b32: D = (D & ~mask) | data), so lanes that share a dword do not race
+__device__ inline void sc_lds_put(uint32_t a, uint4 v, uint32_t len) {
+  const uint32_t sh = a & 3u, wa = a & ~3u;
+  // the len-byte mask as four dwords, then both shifted up by sh bytes into a 20-byte window
+  const uint32_t l0 = len >= 4 ? ~0u : (1u << (8 * len)) - 1;
+  const uint32_t l1 = len >= 8 ? ~0u : (len <= 4 ? 0u : (1u << (8 * (len - 4))) - 1);
+  const uint32_t l2 = len >= 12 ? ~0u : (len <= 8 ? 0u : (1u << (8 * (len - 8))) - 1);
+  const uint32_t l3 = len >= 16 ? ~0u : (len <= 12 ? 0u : (1u << (8 * (len - 12))) - 1);
+  uint32_t u[5], m[5];
+  if (sh == 0) {
+    u[0] = v.x, u[1] = v.y, u[2] = v.z, u[3] = v.w, u[4] = 0;
+    m[0] = l0, m[1] = l1, m[2] = l2, m[3] = l3, m[4] = 0;
+  } else {
+    const uint32_t r = 4 - sh;  // alignbyte(hi, lo, r) = (hi:lo) >> 8r
+    u[0] = v.x << (8 * sh), u[1] = __builtin_amdgcn_alignbyte(v.y, v.x, r), u[2] = __builtin_amdgcn_alignbyte(v.z, v.y, r);
+    u[3] = __builtin_amdgcn_alignbyte(v.w, v.z, r), u[4] = v.w >> (8 * r);
+    m[0] = l0 << (8 * sh), m[1] = __builtin_amdgcn_alignbyte(l1, l0, r), m[2] = __builtin_amdgcn_alignbyte(l2, l1, r);
+    m[3] = __builtin_amdgcn_alignbyte(l3, l2, r), m[4] = l3 >> (8 * r);
+  }
+  asm volatile("ds_mskor_b32 %0, %1, %2" : : "v"(wa), "v"(m[0]), "v"(u[0] & m[0]) : "memory");
+  asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" : : "v"(wa), "v"(m[1]), "v"(u[1] & m[1]) : "memory");
+  if (m[2]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" : : "v"(wa), "v"(m[2]), "v"(u[2] & m[2]) : "memory");
+  if (m[3]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" : : "v"(wa), "v"(m[3]), "v"(u[3] & m[3]) : "memory");
+  if (m[4]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" : : "v"(wa), "v"(m[4]), "v"(u[4] & m[4]) : "memory");
+}
+
+// v shifted up by t (0..3) bytes with the t-byte value tag below it
+__device__ inline uint4 sc_prepend(uint4 v, uint32_t tag, uint32_t t) {
+  if (t == 0) return v;
+  const uint32_t s = 4 - t;  // alignbyte(hi, lo, s) = (hi:lo) >> 8s
+  return make_uint4(__builtin_amdgcn_alignbyte(v.x, tag << (8 * s), s), __builtin_amdgcn_alignbyte(v.y, v.x, s),
+                    __builtin_amdgcn_alignbyte(v.z, v.y, s), __builtin_amdgcn_alignbyte(v.w, v.z, s));
+}
+
+// emit_literal! tag (internal.jl:271-284) for a run of len >= 1 bytes, and its size
+__device__ inline uint32_t sc_lit_tag(uint32_t len, uint32_t& sz) {
+  const uint32_t l1 = len - 1;
+  sz = len <= 60 ? 1u : (len <= 256 ? 2u : 3u);
+  return sz == 1 ? (l1 << 2) : (sz == 2 ? (60u << 2) | (l1 << 8) : (61u << 2) | (l1 << 8));
+}
+
+// one emit_copy_upto_64! piece (internal.jl:289-304), L in 4..64: copy-1 or copy-2, and its size
+__device__ inline uint32_t sc_copy_piece(uint32_t off, uint32_t L, uint32_t& sz) {
+  const bool c1 = L < 12 && off < 2048;
+  sz = c1 ? 2u : 3u;
+  return c1 ? (1u + ((L - 4) << 2) + ((off >> 3) & 0xe0u)) | ((off & 0xffu) << 8) : (2u + ((L - 1) << 2)) | (off << 8);
+}
+
+// A lane's walk over its positions [c0, ce) from s (the reference's greedy loop): copies at match
+// positions, literal runs between them.  Sizes: lead = the first literal run, trail = the last one
+// when the walk ends on literals (the lane has no copies: lead == trail == ce - s), body = the
+// bytes of everything else.  A match position's length byte is 1/2 until the walk first extends it.
+struct ScWalk {
+  uint32_t e, nc, lead, trail, body;
+  uint32_t t0, t1, t2, t3;  // the copies (at most 4 in 16 positions): offset | length << 16 | position << 24
+};
+
+__device__ inline uint32_t sc_extend(const uint8_t* blk, uint32_t q, uint32_t off, uint32_t L, uint32_t cap) {
+  for (;;) {
+    const uint4 x = sc_ld128(blk, q + L), y = sc_ld128(blk, q + L - off);
+    const uint32_t f0 = sc_diff8(x.x, x.y, y.x, y.y);
+    const uint32_t fb = f0 < 8 ? f0 : 8u + sc_diff8(x.z, x.w, y.z, y.w);
+    L = min(L + fb, cap);
+    if (fb < 16 || L >= cap) return L;
+  }
+}
+
+__device__ inline ScWalk sc_walk(const uint8_t* blk, uint8_t* Lp, const uint16_t* Op, uint32_t mask16, uint32_t c0,
+                                 uint32_t ce, uint32_t sce, uint32_t s) {
+  ScWalk w{s, 0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t p = s;
+  bool act = s < ce && s >= c0;  // (lanes past the super-chunk end: ce = c0 > s, nothing to walk)
+  while (ballot(act)) {
+    if (act) {
+      const uint32_t rel = p - c0;
+      const uint32_t m = mask16 >> rel;
+      if (m == 0) {  // literals to the end of the lane's positions
+        const uint32_t run = ce - p;
+        if (w.nc == 0) w.lead = run;
+        w.trail = run;
+        p = ce;
+        act = false;
+      } else {
+        const uint32_t t = (uint32_t)__builtin_ctz(m), q = p + t;
+        if (w.nc == 0)
+          w.lead = t;
+        else if (t)
+          w.body += t + 1;  // an internal run (< 16 bytes: a one-byte tag)
+        const uint32_t i = q - c0;
+        uint32_t L = Lp[i];
+        const uint32_t off = Op[i];
+        if (L < 4) {  // the verified window was full: extend (and keep the result)
+          L = sc_extend(blk, q, off, L == 1 ? 8u : 16u, min(kScMaxL, sce - q));
+          Lp[i] = (uint8_t)L;
+        }
+        w.body += copy_tag_bytes(off, L);
+        const uint32_t tv = off | (L << 16) | (i << 24);
+        w.t0 = w.nc == 0 ? tv : w.t0;
+        w.t1 = w.nc == 1 ? tv : w.t1;
+        w.t2 = w.nc == 2 ? tv : w.t2;
+        w.t3 = w.nc == 3 ? tv : w.t3;
+        ++w.nc;
+        p = q + L;
+        act = p < ce;
+      }
+    }
+  }
+  w.e = s < ce && s >= c0 ? p : s;
+  return w;
+}
+
+// The next block at or after `from` (stride gridDim.x) that the screen left for the parse, or nblk
+// (wave-uniform; 64 candidates per step)
+__device__ inline uint32_t sc_next_block(const CompressArgs& a, uint32_t from, uint32_t lane) {
+  for (uint32_t b0 = from; b0 < a.nblk; b0 += 64 * gridDim.x) {
+    const uint32_t bb = b0 + lane * gridDim.x;
+    const bool todo = bb < a.nblk && (!a.screened || a.out_len[bb] == kScreenTodoSc);
+    const uint64_t m = ballot(todo);
+    if (m) return b0 + ctz64(m) * gridDim.x;
+  }
+  return a.nblk;
+}
+
+// Persistent: one workgroup per CU walks blocks blockIdx.x, + gridDim.x, ...; each wave loads its
+// share of the next block into registers as soon as its last super-chunk is done, so the HBM
+// latency of the staging hides behind the block's tail.
+template <int kDummy>
+__global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
+  __shared__ __attribute__((aligned(16))) ScLds S;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = uniform(tid >> 6);
+  const uint32_t lane = tid & 63;
+  STAMP_DECL
+  constexpr int kPf = kBlockSize / 16 / kScThreads;  // 16-byte pieces per thread of a full block
+  uint4 pf[kPf];
+  // block b's length, source, and whether its bytes are in pf (a 16-byte aligned full block)
+  uint32_t b = sc_next_block(a, blockIdx.x, lane);
+  uint32_t n = 0;
+  const uint8_t* src = nullptr;
+  bool inpf = false;
+  auto fetch = [&](uint32_t bb) {
+    n = bb < a.nblk ? a.in_len[bb] : 0u;
+    src = bb < a.nblk ? a.in + a.in_off[bb] : nullptr;
+    inpf = bb < a.nblk && n == kBlockSize && ((uintptr_t)src & 15) == 0;
+    if (inpf) {
+      const uint4* s16 = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+      for (int i = 0; i < kPf; ++i) pf[i] = s16[tid + i * kScThreads];
+    }
+  };
+  fetch(b);
+  while (b < a.nblk) {
+    uint8_t* const dst = a.out + a.out_off[b];
+    if (n > kBlockSize) {  // (uniform) not a block: error mark, next
+      if (tid == 0) a.out_len[b] = 0xffffffffu;
+      b = sc_next_block(a, b + gridDim.x, lane);
+      fetch(b);
+      continue;
+    }
+    // ---- stage the block, clear the table ----
+    if (inpf) {
+      uint4* d16 = reinterpret_cast<uint4*>(S.blk);
+#pragma unroll
+      for (int i = 0; i < kPf; ++i) d16[tid + i * kScThreads] = pf[i];
+    } else if (((uintptr_t)src & 15) == 0) {
+      const uint4* s16 = reinterpret_cast<const uint4*>(src);
+      uint4* d16 = reinterpret_cast<uint4*>(S.blk);
+      const uint32_t n16 = n >> 4;
+      for (uint32_t k = tid; k < n16; k += kScThreads) d16[k] = s16[k];
+      for (uint32_t k = (n & ~15u) + tid; k < n; k += kScThreads) S.blk[k] = src[k];
+    } else {
+      for (uint32_t k = tid; k < n; k += kScThreads) S.blk[k] = src[k];
+    }
+    if (tid < 64) S.blk[n + tid] = 0;  // bytes past the block read as zeros (never part of a match)
+    {
+      uint4* t16 = reinterpret_cast<uint4*>(S.T);
+      for (uint32_t k = tid; k < (4u << kScTabBits) / 16; k += kScThreads) t16[k] = make_uint4(0, 0, 0, 0);
+    }
+    const uint32_t hv = a.header ? varint_len(n) : 0u;
+    if (tid < hv) dst[tid] = (uint8_t)(((n >> (7 * tid)) & 0x7f) | (tid + 1 < hv ? 0x80 : 0));
+    if (wave == 0) {  // (the previous block's hand-off words were read by wave 0 before the barrier)
+      S.base[lane] = lane == 0 ? hv + 1 : 0u;
+      if (lane == 0) {
+        S.base[64] = 0;
+        S.ins = 0;
+        S.err = 0;
+      }
+    }
+    // the block after this one (its stride scan now, its bytes when this wave is done)
+    const uint32_t bn = sc_next_block(a, b + gridDim.x, lane);
+    __syncthreads();
+    STAMP(8)
+
+  const uint32_t nsc = (n + kScS - 1) / kScS;
+  uint8_t* const Lw = S.L[wave];
+  uint8_t* const Ow = S.O[wave];
+  uint8_t* const Lp = Lw + lane * kScLP;                                       // this lane's slice
+  uint16_t* const Op = reinterpret_cast<uint16_t*>(Ow + lane * kScOP);
+  const uint32_t Tbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)S.T;
+
+  for (uint32_t k = wave; k < nsc; k += kScW) {
+    const uint32_t sc0 = k * kScS, sce = min(sc0 + kScS, n);
+    // ---- A. hashes of the 16 groups: LDS byte address of the bucket, slot value ----
+    uint32_t ha[kScG], hvv[kScG];
+#pragma unroll
+    for (int g = 0; g < (int)kScG; ++g) {
+      const uint32_t q = sc0 + 64 * g + lane;
+      const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, (q & ~3u) + 4), sc_ld32(S.blk, q & ~3u), q & 3u);
+      const uint32_t h = (w * kHashMul) >> (32 - kScTabBits);
+      const bool valid = q + 4 <= n;
+      ha[g] = Tbase + 4 * (valid ? h : (1u << kScTabBits));
+      hvv[g] = (q + 1) << (16 * (g & 1));
+    }
+    const uint32_t mk0 = 0xffffu, mk1 = 0xffff0000u;
+    STAMP(0)
+    STAMP_COUNT(11, 1)
+    // ---- B. the insert token: 16 masked exchanges in position order, then hand it on ----
+    for (uint32_t it = 0; uniform(__hip_atomic_load(&S.ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != k; ++it) {
+      if (it > kScSpinMax) {  // never expected: a broken hand-off must not hang the GPU
+        S.err = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    STAMP(1)
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t tok_a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&S.ins, tok_v = k + 1;
+    uint32_t r[kScG];
+    asm volatile(
+        "ds_mskor_rtn_b32 %0, %16, %32, %34\n"
+        "ds_mskor_rtn_b32 %1, %17, %33, %35\n"
+        "ds_mskor_rtn_b32 %2, %18, %32, %36\n"
+        "ds_mskor_rtn_b32 %3, %19, %33, %37\n"
+        "ds_mskor_rtn_b32 %4, %20, %32, %38\n"
+        "ds_mskor_rtn_b32 %5, %21, %33, %39\n"
+        "ds_mskor_rtn_b32 %6, %22, %32, %40\n"
+        "ds_mskor_rtn_b32 %7, %23, %33, %41\n"
+        "ds_mskor_rtn_b32 %8, %24, %32, %42\n"
+        "ds_mskor_rtn_b32 %9, %25, %33, %43\n"
+        "ds_mskor_rtn_b32 %10, %26, %32, %44\n"
+        "ds_mskor_rtn_b32 %11, %27, %33, %45\n"
+        "ds_mskor_rtn_b32 %12, %28, %32, %46\n"
+        "ds_mskor_rtn_b32 %13, %29, %33, %47\n"
+        "ds_mskor_rtn_b32 %14, %30, %32, %48\n"
+        "ds_mskor_rtn_b32 %15, %31, %33, %49\n"
+        "ds_write_b32 %50, %51\n"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
+          "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
+          "=&v"(r[15])
+        : "v"(ha[0]), "v"(ha[1]), "v"(ha[2]), "v"(ha[3]), "v"(ha[4]), "v"(ha[5]), "v"(ha[6]), "v"(ha[7]), "v"(ha[8]),
+          "v"(ha[9]), "v"(ha[10]), "v"(ha[11]), "v"(ha[12]), "v"(ha[13]), "v"(ha[14]), "v"(ha[15]), "v"(mk0), "v"(mk1),
+          "v"(hvv[0]), "v"(hvv[1]), "v"(hvv[2]), "v"(hvv[3]), "v"(hvv[4]), "v"(hvv[5]), "v"(hvv[6]), "v"(hvv[7]),
+          "v"(hvv[8]), "v"(hvv[9]), "v"(hvv[10]), "v"(hvv[11]), "v"(hvv[12]), "v"(hvv[13]), "v"(hvv[14]),
+          "v"(hvv[15]), "v"(tok_a), "v"(tok_v)
+        : "memory");
+    __builtin_amdgcn_s_setprio(0);
+    STAMP(2)
+
+    // ---- C. verify both candidates of every position ----
+#pragma unroll
+    for (int g = 0; g < (int)kScG; ++g) {
+      const uint32_t q = sc0 + 64 * g + lane;
+      const uint32_t sh = 16 * (g & 1);
+      const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
+      const uint32_t c1 = max(ca, cb), c2 = min(ca, cb);
+      const uint32_t avail = q < sce ? sce - q : 0u;  // bytes a match may cover (super-chunk end)
+      const bool ok1 = avail >= 4 && c1 != 0 && c1 - 1 < q, ok2 = avail >= 4 && c2 != 0 && c2 - 1 < q;
+      const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
+      const uint32_t* wq = reinterpret_cast<const uint32_t*>(S.blk + (q & ~3u));
+      const uint32_t* w1 = reinterpret_cast<const uint32_t*>(S.blk + (p1 & ~3u));
+      const uint32_t* w2 = reinterpret_cast<const uint32_t*>(S.blk + (p2 & ~3u));
+      const uint32_t x0 = wq[0], x1 = wq[1], x2 = wq[2];
+      const uint32_t a0 = w1[0], a1 = w1[1], a2 = w1[2];
+      const uint32_t b0 = w2[0], b1 = w2[1], b2 = w2[2];
+      const uint32_t sq = q & 3u, s1 = p1 & 3u, s2 = p2 & 3u;
+      const uint32_t X0 = __builtin_amdgcn_alignbyte(x1, x0, sq), X1 = __builtin_amdgcn_alignbyte(x2, x1, sq);
+      uint32_t l1 = ok1 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(a1, a0, s1), __builtin_amdgcn_alignbyte(a2, a1, s1)) : 0u;
+      uint32_t l2 = ok2 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(b1, b0, s2), __builtin_amdgcn_alignbyte(b2, b1, s2)) : 0u;
+      uint32_t win = 8;
+      // both fill the window: compare the next 8 bytes to choose (the longer match wins)
+      const bool both = l1 == 8 && l2 == 8 && avail > 8;
+      if (ballot(both)) {
+        if (both) {
+          const uint32_t x3 = wq[3], x4 = wq[4], a3 = w1[3], a4 = w1[4], b3 = w2[3], b4 = w2[4];
+          const uint32_t X2 = __builtin_amdgcn_alignbyte(x3, x2, sq), X3 = __builtin_amdgcn_alignbyte(x4, x3, sq);
+          l1 += sc_diff8(X2, X3, __builtin_amdgcn_alignbyte(a3, a2, s1), __builtin_amdgcn_alignbyte(a4, a3, s1));
+          l2 += sc_diff8(X2, X3, __builtin_amdgcn_alignbyte(b3, b2, s2), __builtin_amdgcn_alignbyte(b4, b3, s2));
+          win = 16;
+        }
+      }
+      const bool take2 = l2 > l1;  // ties: the latest (shorter offset)
+      const uint32_t l = take2 ? l2 : l1, c = take2 ? p2 : p1;
+      const uint32_t L = min(l, avail);
+      const bool match = L >= 4;
+      const bool ext = l == win && avail > win;  // the window was full: the walk extends it
+      const uint32_t enc = !match ? 0u : (ext ? win >> 3 : L);
+      const uint32_t pos = 64 * g + lane;  // in the super-chunk: lane slice pos / 16, entry pos % 16
+      Lw[(pos >> 4) * kScLP + (pos & 15)] = (uint8_t)enc;
+      reinterpret_cast<uint16_t*>(Ow + (pos >> 4) * kScOP)[pos & 15] = (uint16_t)(q - c);
+      const uint64_t mb = ballot(match);
+      if (lane == 0) S.M[wave][g] = mb;
+    }
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    STAMP(3)
+
+    // ---- D. lane-serial walks, resynchronised ----
+    const uint32_t c0 = sc0 + kScC * lane;
+    const uint32_t ce = c0 < sce ? min(c0 + kScC, sce) : c0;
+    const uint32_t mask16 = reinterpret_cast<const uint16_t*>(S.M[wave])[lane];
+    uint32_t s = c0;
+    ScWalk W = sc_walk(S.blk, Lp, Op, mask16, c0, ce, sce, s);
+    for (;;) {
+      const uint32_t pe = __builtin_amdgcn_update_dpp(0u, W.e, 0x138, 0xf, 0xf, false);  // wave_shr:1
+      const uint32_t sn = lane == 0 ? sc0 : pe;
+      const bool chg = sn != s;
+      if (!ballot(chg)) break;
+      STAMP_COUNT(10, 1)
+      if (chg) s = sn;
+      const ScWalk W2 = sc_walk(S.blk, Lp, Op, mask16, c0, ce, sce, chg ? s : ce);
+      if (chg) W = W2;
+    }
+
+    STAMP(4)
+    // ---- E. literal runs across lanes, sizes, offsets ----
+    const uint32_t ptrail = __builtin_amdgcn_update_dpp(0u, W.trail, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane 0: 0)
+    const bool cont = ptrail > 0 && W.lead > 0;  // this lane's first run continues the previous lane's last one
+    const bool mid = cont && W.nc == 0;           // ... and is all the lane has: the run goes on
+    const uint32_t Cs = scan_dpp(cont ? W.lead : 0u);
+    uint32_t f = mid ? 64u : lane;  // first lane >= this one where a run stops passing through
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t o2 = __shfl_down(f, d, 64);
+      f = lane + d < 64 ? min(f, o2) : f;
+    }
+    uint32_t fn = __shfl_down(f, 1, 64);
+    fn = (lane == 63 || fn > 63) ? 63u : fn;
+    const uint32_t Cf = __shfl(Cs, fn, 64);
+    const bool starts = W.trail > 0 && !mid;
+    const uint32_t merged = starts ? W.trail + Cf - Cs : 0u;  // the run this lane's last run starts
+    uint32_t mts;
+    (void)sc_lit_tag(merged ? merged : 1u, mts);
+    uint32_t size;
+    if (W.nc == 0)
+      size = W.lead == 0 ? 0u : (cont ? W.lead : mts + W.trail);
+    else
+      size = (W.lead ? (cont ? W.lead : 1u + W.lead) : 0u) + W.body + (W.trail ? mts + W.trail : 0u);
+    const uint32_t incl = scan_dpp(size);
+    const uint32_t total = readlane(incl, 63);
+
+    STAMP(5)
+    // ---- G1. the lanes' tokens into the wave's staging buffer (its offset slices: their last
+    // reads are done -- the tokens are in registers) ----
+    uint8_t* const stg = Ow;
+    const uint32_t stga = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)stg;
+    {
+      const bool live = s < ce && s >= c0;
+      uint32_t at = stga + incl - size, p = s;
+      const uint32_t tk[4] = {W.t0, W.t1, W.t2, W.t3};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if ((uint32_t)j < W.nc) {
+          const uint32_t tv = tk[j];
+          const uint32_t q = c0 + (tv >> 24), L = (tv >> 16) & 0xffu, off = tv & 0xffffu;
+          const uint32_t run = q - p;  // < 16
+          if (run) {
+            const bool tagged = !(j == 0 && cont);
+            const uint32_t ts = tagged ? 1u : 0u;
+            sc_lds_put(at, sc_prepend(sc_ld128(S.blk, p), (run - 1) << 2, ts), ts + run);
+            at += ts + run;
+          }
+          if (L <= 64) {
+            uint32_t cs;
+            const uint32_t cv = sc_copy_piece(off, L, cs);
+            sc_lds_put(at, make_uint4(cv, 0, 0, 0), cs);
+            at += cs;
+          } else {  // emit_copy! (internal.jl:306-329): 64-byte pieces while >= 68, a 60 if > 64, the rest
+            uint32_t R = L;
+            while (R >= 68) {
+              sc_lds_put(at, make_uint4((2u + (63u << 2)) | (off << 8), 0, 0, 0), 3);
+              at += 3;
+              R -= 64;
+            }
+            if (R > 64) {
+              sc_lds_put(at, make_uint4((2u + (59u << 2)) | (off << 8), 0, 0, 0), 3);
+              at += 3;
+              R -= 60;
+            }
+            uint32_t cs;
+            const uint32_t cv = sc_copy_piece(off, R, cs);
+            sc_lds_put(at, make_uint4(cv, 0, 0, 0), cs);
+            at += cs;
+          }
+          p = q + L;
+        }
+      }
+      if (live && p < ce) {  // the lane's last run: it starts the merged run, unless it only continues one
+        const uint32_t run = ce - p;
+        uint32_t tag = 0, ts = 0;
+        if (!(W.nc == 0 && cont)) tag = sc_lit_tag(merged, ts);
+        sc_lds_put(at, sc_prepend(sc_ld128(S.blk, p), tag, ts), min(ts + run, 16u));
+        if (ts + run > 16) sc_lds_put(at + 16, sc_ld128(S.blk, p + 16 - ts), ts + run - 16);
+      }
+    }
+    STAMP(6)
+
+    // ---- F. the super-chunk's place in the output ----
+    uint32_t bk;
+    for (uint32_t it = 0; (bk = uniform(__hip_atomic_load(&S.base[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) == 0; ++it) {
+      if (it > kScSpinMax) {
+        S.err = 1;
+        bk = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) __hip_atomic_store(&S.base[k + 1], bk + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+
+    // ---- G2. staging -> global: aligned 16-byte stores, bytes at the two partial ends ----
+    {
+      uint8_t* const g = dst + (bk - 1);
+      const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
+      const uint32_t u0 = ad ? 1u : 0u, u1 = (total + ad) >> 4;  // full units [u0, u1); unit u = bytes [16u - ad, +16)
+      uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
+      const uint4* const s16 = reinterpret_cast<const uint4*>(stg);
+      const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;  // a unit starts sb bytes into a staging unit
+      for (uint32_t u = u0 + lane; u < u1; u += 64) {
+        const uint32_t j = 16 * u - ad;  // staging offset of the unit
+        const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
+        const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+        uint32_t r5[5];
+#pragma unroll
+        for (int t = 0; t < 5; ++t) {
+          uint32_t vv = x[t];
+#pragma unroll
+          for (int d = 1; d < 4; ++d) vv = dw == (uint32_t)d ? x[t + d] : vv;
+          r5[t] = vv;
+        }
+        g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
+                            __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
+      }
+      const uint32_t nh = min(u0 ? 16 - ad : 0u, total);           // head bytes [0, nh)
+      const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);  // tail bytes [tb, total)
+      const uint32_t nt = total - tb;
+      if (lane < nh + nt) {
+        const uint32_t jj = lane < nh ? lane : tb + (lane - nh);
+        g[jj] = stg[jj];
+      }
+    }
+    STAMP(7)
+  }
+  fetch(bn);  // the next block's bytes, in flight behind the other waves' last super-chunks
+  __syncthreads();
+  STAMP(9)
+  if (wave == 0) {  // this block's result, read before wave 0 re-initialises the hand-off words
+    const uint32_t fin = S.base[nsc], er = S.err;
+    if (lane == 0) a.out_len[b] = er ? 0xffffffffu : fin - 1;
+  }
+  b = bn;
+  }
+  STAMP_FLUSH(g_stamp_sc)
+}
+
+#if SM_STAMP
+extern "C" int sm_debug_stamps_sc(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_sc), sizeof(g_stamp_sc)) != hipSuccess) return -1;
+  if (reset) {
+    unsigned long long z[12] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_sc), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
+
+hipError_t launch_compress_sc(const CompressArgs& a, hipStream_t s) {
+  static uint32_t ncu_cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  uint32_t ncu = __atomic_load_n(&ncu_cache[dev], __ATOMIC_RELAXED);
+  if (!ncu) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    ncu = (uint32_t)v;
+    __atomic_store_n(&ncu_cache[dev], ncu, __ATOMIC_RELAXED);
+  }
+  const uint32_t grid = min(a.nblk, ncu);  // one workgroup per CU (the LDS holds one)
+  hipLaunchKernelGGL(k_compress_sc<0>, dim3(grid), dim3(kScThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace sm
