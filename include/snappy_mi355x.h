@@ -81,7 +81,8 @@ void sm_ctx_destroy(sm_ctx* ctx);
 void* sm_ctx_stream(sm_ctx* ctx);
 /* diagnostic: how the ctx's last sm_uncompress decoded -- 0 in stream order (one wave),
  * 1 as parallel 64 KiB fragments (a large block-structured stream), 2 in parallel by origin
- * pointers (a large stream whose copies cross 64 KiB blocks), -1 none yet */
+ * pointers (a large stream whose copies cross 64 KiB blocks), 3 a large stream's first error
+ * found in parallel (per-tag checks over its tag path), -1 none yet */
 int sm_ctx_last_path(sm_ctx* ctx);
 
 /* ---- single buffer, host memory (the reference's exported API) -------------------- */
@@ -167,7 +168,9 @@ sm_status sm_uncompress_batch_sharded(sm_ctx* const* ctxs, int nctx, const uint8
 sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, size_t compressed_length);
 
 /* ---- snappy-c.h-shaped entry points, no ctx (a process-wide default context) ---------
- * Same argument shapes and status meaning as libsnappy's snappy-c.h, i.e. exactly the ccall
+ * Same argument shapes and statuses as libsnappy's snappy-c.h: 0 OK, 1 INVALID_INPUT (every
+ * error, device and argument failures included), 2 BUFFER_TOO_SMALL -- the detailed codes
+ * (the reference's messages, SM_ERR_*) come from the ctx API.  That is exactly the ccall
  * signature the reference's helper binds (test/libsnappy.jl:5-30:
  * (Ptr{UInt8}, Csize_t, Ptr{UInt8}, Ref{Csize_t}) -> Cint), so a Julia binding switches from
  * libsnappy by library and symbol name alone.  The default context is created on first use on

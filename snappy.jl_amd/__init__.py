@@ -248,7 +248,8 @@ def find_match_length(buf, i1, i2, limit):
 
 def last_uncompress_path(device=0):
     """How the last uncompress() on this device decoded: 0 in order, 1 parallel fragments
-    (block-structured stream), 2 parallel by origin pointers (copies cross 64 KiB blocks)."""
+    (block-structured stream), 2 parallel by origin pointers (copies cross 64 KiB blocks), 3 a
+    large stream's first error found in parallel (its status returned, no output)."""
     return int(lib().sm_ctx_last_path(context(device)))
 
 

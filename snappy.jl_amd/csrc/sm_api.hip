@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <atomic>
 #include <mutex>
 #include <new>
 #include <thread>
@@ -121,6 +122,7 @@ struct HostTrace {
 #endif
 
 constexpr uint32_t kParallelMinOutput = 4 * 65536;  // smaller streams: one wave is as fast
+constexpr size_t kOrgKeep = 256u << 20;  // origin-pointer scratch a context keeps after a decode
 constexpr size_t kPipeMinInput = 32u << 20;  // sm_compress: inputs this large upload in pieces
 constexpr uint32_t kPieceFrags = 256;        // 16 MiB per piece
 #ifndef SM_OUT_PIECE
@@ -171,13 +173,54 @@ void host_walk(const uint8_t* comp, uint32_t n, uint64_t p, uint64_t lim, uint64
   *produced = o;
 }
 
+// The first error of a stream whose tag path is known: one wave per path element checks its tags
+// (k_path_check), and the first failing element in path order holds the reference's status.  With
+// no failing tag the stream is short of its declared length (Snappy.jl:50).  Returns 3 with *err
+// set, 0 to fall back to the in-order decode, -1 on a device error.
+struct PathChunk {
+  uint64_t y, O, out, ex;
+};
+int path_first_error(sm_ctx* ctx, uint32_t n, uint32_t size, const std::vector<PathChunk>& path, int32_t* err) {
+  if (n >= 0x80000000u || path.empty()) return 0;
+  hipStream_t s = ctx->stream;
+  const size_t npath = path.size();
+  std::vector<sm::OriginPath> op(npath);
+  for (size_t e = 0; e < npath; ++e) {
+    // an element past 2^32 of output is past any declared size: its O saturates (it fails its checks)
+    const uint64_t O = std::min<uint64_t>(path[e].O, 0xffffffffull), out = std::min<uint64_t>(path[e].out, 0xffffffffull - O);
+    op[e] = {(uint32_t)path[e].y, (uint32_t)std::min<uint64_t>(path[e].ex, 0xffffffffull), (uint32_t)O, (uint32_t)out};
+  }
+  const size_t st_off = align_up(npath * sizeof(sm::OriginPath), 256);
+  if (ctx->org.ensure(st_off + npath * 4) != hipSuccess) return 0;
+  sm::OriginPath* d_path = (sm::OriginPath*)ctx->org.p;
+  int32_t* d_st = (int32_t*)((uint8_t*)ctx->org.p + st_off);
+  if (hipMemcpyAsync(d_path, op.data(), npath * sizeof(sm::OriginPath), hipMemcpyHostToDevice, s) != hipSuccess)
+    return -1;
+  if (sm::launch_path_check((const uint8_t*)ctx->in.p, n, size, d_path, (uint32_t)npath, d_st, s) != hipSuccess)
+    return -1;
+  std::vector<int32_t> st(npath);
+  if (hipMemcpyAsync(st.data(), d_st, npath * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  for (int32_t v : st) {
+    if (v == sm::kOk) continue;
+    if (v == sm::kErrCross) return 0;  // the tags do not tile an element: let the in-order decode decide
+    *err = v;
+    return 3;
+  }
+  const PathChunk& last = path.back();
+  if (last.O + last.out == size) return 0;  // no failing tag and the right length: not an error after all
+  *err = sm::kErrInvalid;  // Snappy.jl:50
+  return 3;
+}
+
 // One large stream in parallel (sm_decompress.hip, "one large stream"): index pass, true path
 // on the host, one wave per 64 KiB fragment.  The compressed bytes are in ctx->in.  Returns
-// 1 with the output in ctx->out, 0 to fall back to the in-order decode, -1 on a device error.
-// With host_out, a large output goes down in pieces on the copy stream as the fragment decode
-// finishes them (*copied = true: host_out holds the result when 1 is returned).
+// 1 (or 2, origin pointers) with the output in ctx->out, 3 with *err when the stream has an
+// error (its first one in stream order), 0 to fall back to the in-order decode, -1 on a device
+// error.  With host_out, a large output goes down in pieces on the copy stream as the fragment
+// decode finishes them (*copied = true: host_out holds the result when 1 is returned).
 int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t ip0, uint32_t size,
-                        uint8_t* host_out, bool* copied) {
+                        uint8_t* host_out, bool* copied, int32_t* err) {
   *copied = false;
   using sm::kIdxChunk;
   using sm::kIdxEntries;
@@ -186,7 +229,7 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   const size_t rec_n = (size_t)nchunks * kIdxEntries;
   const size_t frag_off = align_up(2 * rec_n * 4, 16);
   const size_t st_off = frag_off + (size_t)nfrag * sizeof(sm::StreamFrag);
-  if (ctx->idx.ensure(st_off + (size_t)nfrag * 4) != hipSuccess) return -1;
+  if (ctx->idx.ensure(st_off + (size_t)nfrag * 4) != hipSuccess) return 0;  // (the in-order decode needs no scratch)
   hipStream_t s = ctx->stream;
   HT_DECL
   uint32_t* d_rec = (uint32_t*)ctx->idx.p;
@@ -195,15 +238,12 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   HT("index kernel")
   // the index records (8 B per entry, ~9 MB per 64 MiB of stream) come back through the
   // context's pinned staging: one DMA, no page faults, no zero fill
-  if (ctx->stage.ensure(2 * rec_n * 4) != hipSuccess) return -1;
+  if (ctx->stage.ensure(2 * rec_n * 4) != hipSuccess) return 0;
   const uint32_t* rec = (const uint32_t*)ctx->stage.p;
   if (hipMemcpyAsync(ctx->stage.p, d_rec, 2 * rec_n * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
   HT("index records D2H")
   // true path: chunk entries y, output before them O, output of their tags
-  struct PathChunk {
-    uint64_t y, O, out, ex;
-  };
   std::vector<PathChunk> path;
   path.reserve(nchunks + 16);
   uint64_t y = ip0, O = 0;
@@ -220,10 +260,11 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
     }
     path.push_back({y, O, ot, ex});
     O += ot;
-    if (O > size || ex <= y) return 0;
+    if (ex <= y) return 0;
     y = ex;
+    if (O > size) break;  // a tag of this element (or an earlier one) fails: find the first
   }
-  if (O != size) return 0;
+  if (O != size) return path_first_error(ctx, n, size, path, err);
   std::vector<sm::StreamFrag> frags(nfrag);
   size_t k = 0;
   for (uint32_t f = 0; f < nfrag; ++f) {
@@ -262,7 +303,7 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   bool cross = false;
   for (int32_t v : st) {
     if (v == sm::kErrCross) cross = true;
-    else if (v != sm::kOk) return 0;  // an error: the in-order decode reports it exactly
+    else if (v != sm::kOk) return path_first_error(ctx, n, size, path, err);  // the first error, in parallel
   }
   if (!cross) {
     *copied = npiece > 1;
@@ -277,7 +318,7 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
     op[e] = {(uint32_t)path[e].y, (uint32_t)path[e].ex, (uint32_t)path[e].O, (uint32_t)path[e].out};
   const size_t p_off = 0, path_off = align_up((size_t)size * 4, 256), st2_off = align_up(path_off + npath * 16, 256);
   const size_t pend_off = align_up(st2_off + npath * 4, 256);
-  if (ctx->org.ensure(pend_off + 16) != hipSuccess) return -1;
+  if (ctx->org.ensure(pend_off + 16) != hipSuccess) return 0;  // (4 B per output byte: the in-order decode needs none)
   uint8_t* ob = (uint8_t*)ctx->org.p;
   uint32_t* d_P = (uint32_t*)(ob + p_off);
   sm::OriginPath* d_path = (sm::OriginPath*)(ob + path_off);
@@ -290,7 +331,7 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   if (hipMemcpyAsync(st2.data(), d_st2, npath * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
   for (int32_t v : st2)
-    if (v != sm::kOk) return 0;
+    if (v != sm::kOk) return path_first_error(ctx, n, size, path, err);
   // round k moves every unresolved pointer >= 2^k chain steps: 32 rounds cover any size
   bool done = false;
   for (int round = 0; round < 32 && !done; ++round) {
@@ -303,6 +344,10 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   }
   if (!done) return 0;
   if (sm::launch_origin_gather(d_in, d_P, size, (uint8_t*)ctx->out.p, s) != hipSuccess) return -1;
+  if (ctx->org.cap > kOrgKeep) {  // 4 B per output byte: do not keep gigabytes in the context
+    if (hipStreamSynchronize(s) != hipSuccess) return -1;
+    ctx->org.release();
+  }
   return 2;
 }
 
@@ -843,9 +888,14 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   (void)sm_parse32((const uint8_t*)compressed, n, 0, &size, &hdr);
   if (size >= kParallelMinOutput && n - hdr >= 2 * sm::kIdxChunk) {
     bool copied = false;
+    int32_t err = SM_OK;
     const int r = parallel_uncompress(ctx, (const uint8_t*)compressed, (uint32_t)n, (uint32_t)hdr, size,
-                                      (uint8_t*)uncompressed, &copied);
+                                      (uint8_t*)uncompressed, &copied, &err);
     if (r < 0) return SM_ERR_DEVICE;
+    if (r == 3) {  // the stream's first error, found in parallel (the reference throws: no output)
+      ctx->last_path = 3;
+      return err;
+    }
     if (r >= 1) {
       ctx->last_path = r;
       if (!copied) {
@@ -900,7 +950,7 @@ sm_status sm_uncompress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const
 namespace {
 std::mutex g_default_mu;
 sm_ctx* g_default_ctx = nullptr;
-int g_default_mode = SM_MODE_FAST;
+std::atomic<int> g_default_mode{SM_MODE_FAST};  // set and read from any thread
 
 sm_ctx* default_ctx() {
   std::lock_guard<std::mutex> lk(g_default_mu);
@@ -912,35 +962,44 @@ sm_ctx* default_ctx() {
 }
 }  // namespace
 
+namespace {
+// snappy-c.h knows three statuses: 0 OK, 1 INVALID_INPUT, 2 BUFFER_TOO_SMALL.  The detailed codes
+// (the reference's messages 16-21, device and argument failures) stay on the ctx API.
+sm_status snappy_c_status(sm_status st) {
+  return st == SM_OK ? SM_OK : (st == SM_BUFFER_TOO_SMALL ? SM_BUFFER_TOO_SMALL : SM_INVALID_INPUT);
+}
+}  // namespace
+
 sm_status sm_snappy_set_mode(int mode) {
   if (!valid_mode(mode)) return SM_ERR_ARGUMENT;
-  g_default_mode = mode;
+  g_default_mode.store(mode, std::memory_order_relaxed);
   return SM_OK;
 }
 
 sm_status sm_snappy_compress(const char* input, size_t input_length, char* compressed, size_t* compressed_length) {
   sm_ctx* ctx = default_ctx();
-  if (!ctx) return SM_ERR_DEVICE;
-  return sm_compress(ctx, input, input_length, compressed, compressed_length, g_default_mode);
+  if (!ctx) return SM_INVALID_INPUT;
+  return snappy_c_status(sm_compress(ctx, input, input_length, compressed, compressed_length,
+                                     g_default_mode.load(std::memory_order_relaxed)));
 }
 
 sm_status sm_snappy_uncompress(const char* compressed, size_t compressed_length, char* uncompressed,
                                size_t* uncompressed_length) {
   sm_ctx* ctx = default_ctx();
-  if (!ctx) return SM_ERR_DEVICE;
-  return sm_uncompress(ctx, compressed, compressed_length, uncompressed, uncompressed_length);
+  if (!ctx) return SM_INVALID_INPUT;
+  return snappy_c_status(sm_uncompress(ctx, compressed, compressed_length, uncompressed, uncompressed_length));
 }
 
 size_t sm_snappy_max_compressed_length(size_t source_length) { return sm_max_compressed_length(source_length); }
 
 sm_status sm_snappy_uncompressed_length(const char* compressed, size_t compressed_length, size_t* result) {
-  return sm_uncompressed_length(compressed, compressed_length, result);
+  return snappy_c_status(sm_uncompressed_length(compressed, compressed_length, result));
 }
 
 sm_status sm_snappy_validate_compressed_buffer(const char* compressed, size_t compressed_length) {
   sm_ctx* ctx = default_ctx();
-  if (!ctx) return SM_ERR_DEVICE;
-  return sm_validate_compressed_buffer(ctx, compressed, compressed_length);
+  if (!ctx) return SM_INVALID_INPUT;
+  return snappy_c_status(sm_validate_compressed_buffer(ctx, compressed, compressed_length));
 }
 
 }  // extern "C"

@@ -90,13 +90,15 @@ constexpr uint32_t kTabBytes = 2 * kMaxHashTableSize;
 // measured on gfx950, tools/probes/buffer_range.hip).  word(pos) therefore loads at
 // min(pos, n - 4) and shifts, so the bytes below n are exact and the bytes past it read 0
 // (the zero slack the reference's find_match_length never compares) -- and no load touches
-// memory past the block.
+// memory past the block.  A position at or past n (a shift of 32 or more) gives 0 explicitly:
+// such a shift is undefined in C++, and the hardware's v_lshrrev would mask it to 5 bits.
 struct BlockBytes {
   __amdgpu_buffer_rsrc_t r;
   uint32_t nm4;  // n - 4 (word() is used only when n >= 15)
   __device__ uint32_t word(uint32_t pos) const {
-    const uint32_t pc = min(pos, nm4);
-    return __builtin_amdgcn_raw_buffer_load_b32(r, (int)pc, 0, 0) >> ((pos - pc) << 3);
+    const uint32_t pc = min(pos, nm4), sh = pos - pc;  // sh: 0..3 below n, >= 4 at or past n
+    const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(r, (int)pc, 0, 0);
+    return sh < 4 ? w >> (sh << 3) : 0u;
   }
   __device__ uint32_t byte(uint32_t pos) const { return __builtin_amdgcn_raw_buffer_load_b8(r, (int)pos, 0, 0); }
 };

@@ -7,28 +7,29 @@
 // insert of ALL positions (not only the probed ones), and the block is cut into 1 KiB
 // super-chunks whose copies stop at the super-chunk end.
 //
-// One 16-wave workgroup per block; the block (64 KiB) and a 32 KiB hash table live in LDS.  Wave w
-// owns super-chunks w, w + 16, ... (64 positions per lane-group, 16 groups).  Per super-chunk:
-//  A. hash its 16 groups of 64 positions (the reference's multiply, internal.jl:94, 13 bits);
-//  B. wait for the insert token, then ONE ds_mskor_rtn_b32 per group exchanges the positions into
+// Persistent: one 16-wave workgroup per CU walks its blocks; the block (64 KiB) and a 32 KiB hash
+// table live in LDS.  A wave takes the next super-chunk of the block from an LDS counter and:
+//  A. hashes its 16 groups of 64 positions (the reference's multiply, internal.jl:94, 13 bits);
+//  B. waits for the insert token, then ONE ds_mskor_rtn_b32 per group exchanges the positions into
 //     the table and hands the token on.  A table dword holds two u16 slots (position + 1): group
 //     parity g & 1 picks the slot a position is written to, and the returned dword gives both
 //     candidates at once -- the latest earlier position of the same hash in the own slot (exact:
 //     a wave's LDS instructions execute in order, and the conflicting lanes of one instruction in
 //     ascending lane order) and the latest one of the other parity.  Correctness never depends on
 //     that order (every candidate is verified); only the ratio does;
-//  C. verify both candidates (8 bytes, then 16 where both fill 8), keep the longer, and store per
-//     position the match length (u8; 1/2 = "extend from 8/16") and offset (u16) in the wave's
-//     lane slices, plus the match bitmask;
-//  D. each LANE walks the 16 positions it owns greedily and serially (the reference's loop:
-//     literal runs are skipped through the bitmask, a match is extended 16 bytes a step up to 255
-//     bytes).  A copy can end inside a later lane's positions, so the walks are resynchronised:
-//     every lane starts at its first position, then lanes whose true start (the previous lane's
-//     end) differs walk again, until no start changes;
+//  C. verifies both candidates (8 bytes, then 16 where both fill 8), keeps the longer, and stores
+//     per position the match length (u8; 1/2 = "extend from 8/16") and offset (u16), position-
+//     major so that a lane's 16 positions are one aligned 16-byte row, plus the match bitmask;
+//  D. each LANE loads its row into registers and walks its 16 positions greedily and serially (the
+//     reference's loop: literal runs skipped through the bitmask, a match extended 16 bytes a step
+//     up to 255 bytes).  A copy can end inside a later lane's positions, so the walks are
+//     resynchronised: every lane starts at its first position; a lane whose true start (the previous
+//     lane's end) differs walks from there until it lands on its old path, and keeps the old tokens
+//     from that point on; repeated until no start changes;
 //  E. literal runs that cross lanes get one tag (segmented scan), token sizes, a DPP scan;
+//  G1. the lanes write their tokens into an LDS staging buffer (masked ors: lanes share dwords);
 //  F. the super-chunk's output offset comes from the previous super-chunk (an LDS word), and
-//  G. each lane writes its tokens straight to global memory (16-byte stores whose tails the same
-//     lane overwrites later; exact stores at the lane's end).
+//  G2. the wave copies the staging buffer out with aligned 16-byte stores.
 // Output is deterministic.
 #include "sm_device.h"
 #include "sm_internal.h"
@@ -43,36 +44,40 @@ constexpr uint32_t kScG = kScS / 64;      // 64-position groups per super-chunk 
 constexpr uint32_t kScW = 16;             // waves per workgroup
 constexpr uint32_t kScThreads = 64 * kScW;
 constexpr uint32_t kScTabBits = 13;       // 8 K dwords = 16 K u16 slots
-constexpr uint32_t kScLP = kScC + 4;      // lane slice pitch of the length bytes (odd dword count: no bank conflicts)
-constexpr uint32_t kScOP = 2 * kScC + 4;  // lane slice pitch of the u16 offsets
 constexpr uint32_t kScMaxL = 255;         // longest copy token (u8 lengths)
 constexpr uint32_t kScMaxSc = kBlockSize / kScS;
 constexpr uint32_t kScSpinMax = 1u << 22;  // hand-off polls (64 cycles each) before a wait gives up
-static_assert(kScC == 16 && kScG == 16, "the walk keeps a lane's 16 positions in one u16 mask");
+static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, one 16-byte row");
 
 #if SM_STAMP
 __device__ unsigned long long g_stamp_sc[12];
 #endif
 STAMP_MACROS(12)
 
-typedef uint4 __attribute__((aligned(1))) sc_u128u;
-typedef uint64_t __attribute__((aligned(1))) sc_u64u;
-typedef uint32_t __attribute__((aligned(1))) sc_u32u;
-typedef uint16_t __attribute__((aligned(1))) sc_u16u;
-
+// per-wave LDS: rows of 16 positions (row r = lane r's positions)
+struct ScWaveLds {
+  uint8_t L[kScS];         // match length byte per position (0: none; 1/2: extend from 8/16)
+  uint16_t Olo[kScS / 2];  // offsets of positions 0..7 of each row
+  uint16_t Ohi[kScS / 2];  // offsets of positions 8..15 of each row (Olo + Ohi: the staging buffer later)
+};
 struct ScLds {
-  uint8_t blk[kBlockSize + 64];             // the block (+ pad: reads run up to 20 bytes past a position)
-  uint32_t T[(1u << kScTabBits) + 4];       // hash table; T[1 << kScTabBits] is the dummy for invalid lanes
-  uint8_t L[kScW][64 * kScLP];              // per wave: match length byte of each position (lane slices)
-  uint8_t O[kScW][64 * kScOP];              // per wave: u16 offset of each position (lane slices)
-  uint64_t M[kScW][kScG];                   // per wave: match bitmask (bit = position of the super-chunk)
-  uint32_t ins;                             // insert token: super-chunks inserted so far
-  uint32_t err;                             // a hand-off wait timed out (never expected)
-  uint32_t base[kScMaxSc + 1];              // output offset of super-chunk k, + 1 (0: not known yet)
+  uint8_t blk[kBlockSize + 64];        // the block (+ pad: reads run up to 20 bytes past a position)
+  uint32_t T[(1u << kScTabBits) + 4];  // hash table; T[1 << kScTabBits] is the dummy for invalid lanes
+  ScWaveLds w[kScW];
+  uint64_t M[kScW][kScG];              // per wave: match bitmask (bit = position of the super-chunk)
+  uint32_t ins;                        // insert token: super-chunks inserted so far
+  uint32_t next;                       // the next super-chunk to take
+  uint32_t err;                        // a hand-off wait timed out (never expected)
+  uint32_t base[kScMaxSc + 1];         // output offset of super-chunk k, + 1 (0: not known yet)
 };
 static_assert(sizeof(ScLds) <= 160 * 1024, "LDS");
+static_assert(sizeof(ScWaveLds) % 16 == 0 && offsetof(ScLds, w) % 16 == 0, "rows are 16-byte aligned");
 
 __device__ inline uint32_t sc_ld32(const uint8_t* blk, uint32_t a) { return *reinterpret_cast<const uint32_t*>(blk + a); }
+
+__device__ inline uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
 
 // 16 bytes of the block at p (five aligned dwords, four funnel shifts)
 __device__ inline uint4 sc_ld128(const uint8_t* blk, uint32_t p) {
@@ -85,41 +90,12 @@ __device__ inline uint4 sc_ld128(const uint8_t* blk, uint32_t p) {
 
 // first differing byte of two 8-byte values given as dword pairs (8: equal)
 __device__ inline uint32_t sc_diff8(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
-  const uint32_t d0 = a0 ^ b0, d1 = a1 ^ b1;
-  return d0 ? (uint32_t)__builtin_ctz(d0) >> 3 : (d1 ? 4u + ((uint32_t)__builtin_ctz(d1) >> 3) : 8u);
+  const uint64_t d = ((uint64_t)(a1 ^ b1) << 32) | (a0 ^ b0);
+  return d ? (uint32_t)__builtin_ctzll(d) >> 3 : 8u;
 }
 
-// len (< 16 unless at + 16 <= oend) low bytes of v to dst[at..]: one 16-byte store when the lane's
-// output continues past it (the tail is garbage that this lane overwrites later), exact otherwise
-__device__ inline void sc_put(uint8_t* dst, uint32_t at, uint4 v, uint32_t len, uint32_t oend) {
-  if (at + 16 <= oend) {
-#pragma clang diagnostic push
-#pragma clang diagnostic ignored "-Walign-mismatch"
-    *reinterpret_cast<sc_u128u*>(dst + at) = v;  // unaligned global stores are served on gfx950
-#pragma clang diagnostic pop
-    return;
-  }
-  uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
-  if (len & 8) {
-    *reinterpret_cast<sc_u64u*>(dst + at) = lo;
-    lo = hi;
-    at += 8;
-  }
-  if (len & 4) {
-    *reinterpret_cast<sc_u32u*>(dst + at) = (uint32_t)lo;
-    lo >>= 32;
-    at += 4;
-  }
-  if (len & 2) {
-    *reinterpret_cast<sc_u16u*>(dst + at) = (uint16_t)lo;
-    lo >>= 16;
-    at += 2;
-  }
-  if (len & 1) dst[at] = (uint8_t)lo;
-}
-
-// bytes v[0, len) (len 1..16) to the LDS byte array at byte address a (any alignment): up to five
-// masked ors (ds_mskor_b32: D = (D & ~mask) | data), so lanes that share a dword do not race
+// bytes v[0, len) (len 1..16) to the LDS byte array at byte address a (any alignment): masked ors
+// (ds_mskor_b32: D = (D & ~mask) | data), so lanes that share a dword do not race
 __device__ inline void sc_lds_put(uint32_t a, uint4 v, uint32_t len) {
   const uint32_t sh = a & 3u, wa = a & ~3u;
   // the len-byte mask as four dwords, then both shifted up by sh bytes into a 20-byte window
@@ -139,10 +115,18 @@ __device__ inline void sc_lds_put(uint32_t a, uint4 v, uint32_t len) {
     m[3] = __builtin_amdgcn_alignbyte(l3, l2, r), m[4] = l3 >> (8 * r);
   }
   asm volatile("ds_mskor_b32 %0, %1, %2" : : "v"(wa), "v"(m[0]), "v"(u[0] & m[0]) : "memory");
-  asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" : : "v"(wa), "v"(m[1]), "v"(u[1] & m[1]) : "memory");
+  if (m[1]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" : : "v"(wa), "v"(m[1]), "v"(u[1] & m[1]) : "memory");
   if (m[2]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" : : "v"(wa), "v"(m[2]), "v"(u[2] & m[2]) : "memory");
   if (m[3]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" : : "v"(wa), "v"(m[3]), "v"(u[3] & m[3]) : "memory");
   if (m[4]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" : : "v"(wa), "v"(m[4]), "v"(u[4] & m[4]) : "memory");
+}
+
+// the cs (2 or 3) low bytes of v to LDS byte address a, byte by byte (a copy tag: these bytes are
+// this lane's alone -- only a piece's first and last dword can be shared, and byte stores do not race)
+__device__ inline void sc_lds_put3(uint8_t* p, uint32_t v, uint32_t cs) {
+  p[0] = (uint8_t)v;
+  p[1] = (uint8_t)(v >> 8);
+  if (cs > 2) p[2] = (uint8_t)(v >> 16);
 }
 
 // v shifted up by t (0..3) bytes with the t-byte value tag below it
@@ -167,15 +151,6 @@ __device__ inline uint32_t sc_copy_piece(uint32_t off, uint32_t L, uint32_t& sz)
   return c1 ? (1u + ((L - 4) << 2) + ((off >> 3) & 0xe0u)) | ((off & 0xffu) << 8) : (2u + ((L - 1) << 2)) | (off << 8);
 }
 
-// A lane's walk over its positions [c0, ce) from s (the reference's greedy loop): copies at match
-// positions, literal runs between them.  Sizes: lead = the first literal run, trail = the last one
-// when the walk ends on literals (the lane has no copies: lead == trail == ce - s), body = the
-// bytes of everything else.  A match position's length byte is 1/2 until the walk first extends it.
-struct ScWalk {
-  uint32_t e, nc, lead, trail, body;
-  uint32_t t0, t1, t2, t3;  // the copies (at most 4 in 16 positions): offset | length << 16 | position << 24
-};
-
 __device__ inline uint32_t sc_extend(const uint8_t* blk, uint32_t q, uint32_t off, uint32_t L, uint32_t cap) {
   for (;;) {
     const uint4 x = sc_ld128(blk, q + L), y = sc_ld128(blk, q + L - off);
@@ -186,53 +161,22 @@ __device__ inline uint32_t sc_extend(const uint8_t* blk, uint32_t q, uint32_t of
   }
 }
 
-__device__ inline ScWalk sc_walk(const uint8_t* blk, uint8_t* Lp, const uint16_t* Op, uint32_t mask16, uint32_t c0,
-                                 uint32_t ce, uint32_t sce, uint32_t s) {
-  ScWalk w{s, 0, 0, 0, 0, 0, 0, 0, 0};
-  uint32_t p = s;
-  bool act = s < ce && s >= c0;  // (lanes past the super-chunk end: ce = c0 > s, nothing to walk)
-  while (ballot(act)) {
-    if (act) {
-      const uint32_t rel = p - c0;
-      const uint32_t m = mask16 >> rel;
-      if (m == 0) {  // literals to the end of the lane's positions
-        const uint32_t run = ce - p;
-        if (w.nc == 0) w.lead = run;
-        w.trail = run;
-        p = ce;
-        act = false;
-      } else {
-        const uint32_t t = (uint32_t)__builtin_ctz(m), q = p + t;
-        if (w.nc == 0)
-          w.lead = t;
-        else if (t)
-          w.body += t + 1;  // an internal run (< 16 bytes: a one-byte tag)
-        const uint32_t i = q - c0;
-        uint32_t L = Lp[i];
-        const uint32_t off = Op[i];
-        if (L < 4) {  // the verified window was full: extend (and keep the result)
-          L = sc_extend(blk, q, off, L == 1 ? 8u : 16u, min(kScMaxL, sce - q));
-          Lp[i] = (uint8_t)L;
-        }
-        w.body += copy_tag_bytes(off, L);
-        const uint32_t tv = off | (L << 16) | (i << 24);
-        w.t0 = w.nc == 0 ? tv : w.t0;
-        w.t1 = w.nc == 1 ? tv : w.t1;
-        w.t2 = w.nc == 2 ? tv : w.t2;
-        w.t3 = w.nc == 3 ? tv : w.t3;
-        ++w.nc;
-        p = q + L;
-        act = p < ce;
-      }
-    }
-  }
-  w.e = s < ce && s >= c0 ? p : s;
-  return w;
-}
+// c ? a : b on values (a conditional on lvalues can become a select of their addresses)
+__device__ inline uint32_t sc_sel(uint32_t c, uint32_t a, uint32_t b) { return c ? a : b; }
+
+// bits [a, b) of a u32 (0 <= a <= b <= 31)
+__device__ inline uint32_t sc_bits(uint32_t a, uint32_t b) { return ((1u << b) - 1u) & ~((1u << a) - 1u); }
+
+// a lane's tokens: the copies of its walk (at most 4 in 16 positions), offset | length << 16 |
+// position-in-row << 24, in position order
+struct ScToks {
+  uint32_t t[4];
+  uint32_t n;
+};
 
 // The next block at or after `from` (stride gridDim.x) that the screen left for the parse, or nblk
 // (wave-uniform; 64 candidates per step)
-__device__ inline uint32_t sc_next_block(const CompressArgs& a, uint32_t from, uint32_t lane) {
+__device__ __attribute__((always_inline)) inline uint32_t sc_next_block(const CompressArgs& a, uint32_t from, uint32_t lane) {
   for (uint32_t b0 = from; b0 < a.nblk; b0 += 64 * gridDim.x) {
     const uint32_t bb = b0 + lane * gridDim.x;
     const bool todo = bb < a.nblk && (!a.screened || a.out_len[bb] == kScreenTodoSc);
@@ -242,8 +186,397 @@ __device__ inline uint32_t sc_next_block(const CompressArgs& a, uint32_t from, u
   return a.nblk;
 }
 
+// One super-chunk, by one wave (sections A-G2 above).
+__device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, const uint32_t k, const uint32_t n, uint8_t* const dst,
+                                     const uint32_t wave, const uint32_t lane) {
+  ScWaveLds& Wl = S.w[wave];
+  const uint32_t sc0 = k * kScS, sce = min(sc0 + kScS, n);
+  const uint32_t Tbase = lds_addr(S.T);
+  STAMP_DECL
+  // ---- A. hashes of the 16 groups: LDS byte address of the bucket, slot value ----
+  uint32_t ha[kScG], hvv[kScG];
+#pragma unroll
+  for (int g = 0; g < (int)kScG; ++g) {
+    const uint32_t q = sc0 + 64 * g + lane;
+    const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, (q & ~3u) + 4), sc_ld32(S.blk, q & ~3u), q & 3u);
+    const uint32_t h = (w * kHashMul) >> (32 - kScTabBits);
+    const bool valid = q + 4 <= n;
+    ha[g] = Tbase + 4 * (valid ? h : (1u << kScTabBits));
+    hvv[g] = (q + 1) << (16 * (g & 1));
+  }
+  const uint32_t mk0 = 0xffffu, mk1 = 0xffff0000u;
+  STAMP(0)
+  STAMP_COUNT(11, 1)
+  // ---- B. the insert token: 16 masked exchanges in position order, then hand it on ----
+  for (uint32_t it = 0; uniform(__hip_atomic_load(&S.ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != k; ++it) {
+    if (it > kScSpinMax) {  // never expected: a broken hand-off must not hang the GPU
+      S.err = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  STAMP(1)
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t tok_a = lds_addr(&S.ins), tok_v = k + 1;
+  uint32_t r[kScG];
+  asm volatile(
+      "ds_mskor_rtn_b32 %0, %16, %32, %34\n"
+      "ds_mskor_rtn_b32 %1, %17, %33, %35\n"
+      "ds_mskor_rtn_b32 %2, %18, %32, %36\n"
+      "ds_mskor_rtn_b32 %3, %19, %33, %37\n"
+      "ds_mskor_rtn_b32 %4, %20, %32, %38\n"
+      "ds_mskor_rtn_b32 %5, %21, %33, %39\n"
+      "ds_mskor_rtn_b32 %6, %22, %32, %40\n"
+      "ds_mskor_rtn_b32 %7, %23, %33, %41\n"
+      "ds_mskor_rtn_b32 %8, %24, %32, %42\n"
+      "ds_mskor_rtn_b32 %9, %25, %33, %43\n"
+      "ds_mskor_rtn_b32 %10, %26, %32, %44\n"
+      "ds_mskor_rtn_b32 %11, %27, %33, %45\n"
+      "ds_mskor_rtn_b32 %12, %28, %32, %46\n"
+      "ds_mskor_rtn_b32 %13, %29, %33, %47\n"
+      "ds_mskor_rtn_b32 %14, %30, %32, %48\n"
+      "ds_mskor_rtn_b32 %15, %31, %33, %49\n"
+      "ds_write_b32 %50, %51\n"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
+        "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]), "=&v"(r[15])
+      : "v"(ha[0]), "v"(ha[1]), "v"(ha[2]), "v"(ha[3]), "v"(ha[4]), "v"(ha[5]), "v"(ha[6]), "v"(ha[7]), "v"(ha[8]),
+        "v"(ha[9]), "v"(ha[10]), "v"(ha[11]), "v"(ha[12]), "v"(ha[13]), "v"(ha[14]), "v"(ha[15]), "v"(mk0), "v"(mk1),
+        "v"(hvv[0]), "v"(hvv[1]), "v"(hvv[2]), "v"(hvv[3]), "v"(hvv[4]), "v"(hvv[5]), "v"(hvv[6]), "v"(hvv[7]),
+        "v"(hvv[8]), "v"(hvv[9]), "v"(hvv[10]), "v"(hvv[11]), "v"(hvv[12]), "v"(hvv[13]), "v"(hvv[14]), "v"(hvv[15]),
+        "v"(tok_a), "v"(tok_v)
+      : "memory");
+  __builtin_amdgcn_s_setprio(0);
+  STAMP(2)
+
+  // ---- C. verify both candidates of every position ----
+#pragma unroll
+  for (int g = 0; g < (int)kScG; ++g) {
+    const uint32_t q = sc0 + 64 * g + lane;
+    const uint32_t sh = 16 * (g & 1);
+    const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
+    const uint32_t c1 = max(ca, cb), c2 = min(ca, cb);
+    const uint32_t avail = q < sce ? sce - q : 0u;  // bytes a match may cover (super-chunk end)
+    // (c - 1 < q also rejects c == 0; only invalid lanes -- avail < 4 -- can see other values)
+    const bool ok1 = avail >= 4 && c1 - 1 < q, ok2 = avail >= 4 && c2 - 1 < q;
+    const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
+    const uint32_t* wq = reinterpret_cast<const uint32_t*>(S.blk + (q & ~3u));
+    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(S.blk + (p1 & ~3u));
+    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(S.blk + (p2 & ~3u));
+    const uint32_t x0 = wq[0], x1 = wq[1], x2 = wq[2];
+    const uint32_t a0 = w1[0], a1 = w1[1], a2 = w1[2];
+    const uint32_t b0 = w2[0], b1 = w2[1], b2 = w2[2];
+    const uint32_t sq = q & 3u, s1 = p1 & 3u, s2 = p2 & 3u;
+    const uint32_t X0 = __builtin_amdgcn_alignbyte(x1, x0, sq), X1 = __builtin_amdgcn_alignbyte(x2, x1, sq);
+    uint32_t l1 = ok1 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(a1, a0, s1), __builtin_amdgcn_alignbyte(a2, a1, s1)) : 0u;
+    uint32_t l2 = ok2 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(b1, b0, s2), __builtin_amdgcn_alignbyte(b2, b1, s2)) : 0u;
+    uint32_t win = 8;
+    // both fill the window: compare the next 8 bytes to choose (the longer match wins)
+    const bool both = l1 == 8 && l2 == 8 && avail > 8;
+    if (ballot(both)) {
+      if (both) {
+        const uint32_t x3 = wq[3], x4 = wq[4], a3 = w1[3], a4 = w1[4], b3 = w2[3], b4 = w2[4];
+        const uint32_t X2 = __builtin_amdgcn_alignbyte(x3, x2, sq), X3 = __builtin_amdgcn_alignbyte(x4, x3, sq);
+        l1 += sc_diff8(X2, X3, __builtin_amdgcn_alignbyte(a3, a2, s1), __builtin_amdgcn_alignbyte(a4, a3, s1));
+        l2 += sc_diff8(X2, X3, __builtin_amdgcn_alignbyte(b3, b2, s2), __builtin_amdgcn_alignbyte(b4, b3, s2));
+        win = 16;
+      }
+    }
+    const bool take2 = l2 > l1;  // ties: the latest (shorter offset)
+    const uint32_t l = take2 ? l2 : l1, c = take2 ? p2 : p1;
+    const uint32_t L = min(l, avail);
+    const bool match = L >= 4;
+    const bool ext = l == win && avail > win;  // the window was full: the walk extends it
+    const uint32_t enc = !match ? 0u : (ext ? win >> 3 : L);
+    const uint32_t pos = 64 * g + lane;  // row pos / 16, entry pos % 16
+    Wl.L[pos] = (uint8_t)enc;
+    uint16_t* const Orow = (lane & 8) ? Wl.Ohi : Wl.Olo;
+    Orow[(pos >> 4) * 8 + (lane & 7)] = (uint16_t)(q - c);
+    const uint64_t mb = ballot(match);
+    if (lane == 0) S.M[wave][g] = mb;
+  }
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  STAMP(3)
+
+  // ---- D. lane-serial walks over the row in registers, resynchronised ----
+  const uint32_t c0 = sc0 + kScC * lane;
+  const uint32_t ce = c0 < sce ? min(c0 + kScC, sce) : c0;
+  const uint32_t mask16 = reinterpret_cast<const uint16_t*>(S.M[wave])[lane];
+  // the row in scalars (a select between aggregates would make the compiler address them in memory)
+  uint32_t l0, l1, l2, l3;
+  {
+    const uint4 v = reinterpret_cast<const uint4*>(Wl.L)[lane];
+    l0 = v.x, l1 = v.y, l2 = v.z, l3 = v.w;
+  }
+  const uint4 Olr = reinterpret_cast<const uint4*>(Wl.Olo)[lane], Ohr = reinterpret_cast<const uint4*>(Wl.Ohi)[lane];
+  const uint32_t o0 = Olr.x, o1 = Olr.y, o2 = Olr.z, o3 = Olr.w, o4 = Ohr.x, o5 = Ohr.y, o6 = Ohr.z, o7 = Ohr.w;
+  auto getL = [&](uint32_t i) -> uint32_t {
+    const uint32_t d = sc_sel(i & 8, sc_sel(i & 4, l3, l2), sc_sel(i & 4, l1, l0));
+    return (d >> (8 * (i & 3))) & 0xffu;
+  };
+  auto setL = [&](uint32_t i, uint32_t v) {  // (after an extension: later walks of this super-chunk reuse it)
+    const uint32_t sb = 8 * (i & 3), m = ~(0xffu << sb), x = v << sb, j = i >> 2;
+    l0 = j == 0 ? (l0 & m) | x : l0;
+    l1 = j == 1 ? (l1 & m) | x : l1;
+    l2 = j == 2 ? (l2 & m) | x : l2;
+    l3 = j == 3 ? (l3 & m) | x : l3;
+  };
+  auto getO = [&](uint32_t i) -> uint32_t {
+    const uint32_t hi = i & 8;
+    const uint32_t hx = sc_sel(hi, o4, o0), hy = sc_sel(hi, o5, o1), hz = sc_sel(hi, o6, o2), hw = sc_sel(hi, o7, o3);
+    const uint32_t d = sc_sel(i & 4, sc_sel(i & 2, hw, hz), sc_sel(i & 2, hy, hx));
+    return (d >> (16 * (i & 1))) & 0xffffu;
+  };
+  // Walk from s (c0 <= s < ce) until the walk lands on a position of `stop` (the lane's old path)
+  // or leaves the row: new tokens in nt, the path positions in newP, the end (or merge) position.
+  auto walk = [&](uint32_t s, uint32_t stop, ScToks& nt, uint32_t& newP, uint32_t& pend, bool& merged) __attribute__((always_inline)) {
+    nt.n = 0;
+    nt.t[0] = nt.t[1] = nt.t[2] = nt.t[3] = 0;
+    newP = 0;
+    merged = false;
+    uint32_t p = s;
+    bool act = true;
+    while (ballot(act)) {
+      if (act) {
+        const uint32_t rel = p - c0;
+        const uint32_t m = mask16 >> rel;
+        const uint32_t t = m ? (uint32_t)__builtin_ctz(m) : ce - p;  // literals before the next match
+        const uint32_t sb = (stop >> rel) & ((2u << t) - 1u);         // old-path positions in [p, p + t]
+        if (sb) {  // lands on the old path: from here the walks are the same
+          const uint32_t d = (uint32_t)__builtin_ctz(sb);
+          newP |= sc_bits(rel, rel + d);
+          p += d;
+          merged = true;
+          act = false;
+        } else if (!m) {  // literals to the end of the row
+          newP |= sc_bits(rel, ce - c0);
+          p = ce;
+          act = false;
+        } else {
+          const uint32_t i = rel + t;
+          newP |= sc_bits(rel, i + 1);
+          uint32_t L = getL(i);
+          const uint32_t off = getO(i);
+          if (L < 4) {  // the verified window was full: extend
+            L = sc_extend(S.blk, c0 + i, off, L == 1 ? 8u : 16u, min(kScMaxL, sce - (c0 + i)));
+            setL(i, L);
+          }
+          const uint32_t tv = off | (L << 16) | (i << 24);
+          nt.t[0] = nt.n == 0 ? tv : nt.t[0];
+          nt.t[1] = nt.n == 1 ? tv : nt.t[1];
+          nt.t[2] = nt.n == 2 ? tv : nt.t[2];
+          nt.t[3] = nt.n == 3 ? tv : nt.t[3];
+          ++nt.n;
+          p = c0 + i + L;
+          act = p < ce;
+        }
+      }
+    }
+    pend = p;
+  };
+  const bool row = c0 < sce;  // the lane has positions
+  uint32_t s = c0, e, P;
+  ScToks tk;
+  {
+    bool mg;
+    walk(row ? c0 : ce, 0u, tk, P, e, mg);
+    if (!row) {
+      tk.n = 0;
+      e = c0;
+    }
+  }
+  for (;;) {
+    const uint32_t pe = __builtin_amdgcn_update_dpp(0u, e, 0x138, 0xf, 0xf, false);  // wave_shr:1
+    const uint32_t sn = lane == 0 ? sc0 : pe;
+    const bool chg = sn != s;
+    if (!ballot(chg)) break;
+    STAMP_COUNT(10, 1)
+    const bool inrow = chg && sn >= c0 && sn < ce;
+    ScToks nt;
+    uint32_t nP, m;
+    bool mg;
+    walk(inrow ? sn : ce, P & ~sc_bits(0, inrow ? sn - c0 : 0), nt, nP, m, mg);  // (rows not walking: stop at once)
+    if (chg) {
+      s = sn;
+      if (!inrow) {  // past the row (a copy jumped over it) or a lane without positions
+        tk.n = 0;
+        P = 0;
+        e = sn;
+      } else if (!mg) {
+        tk = nt;
+        P = nP;
+        e = m;
+      } else {  // the new tokens, then the old ones from the merge position on (e unchanged)
+        const uint32_t mi = m - c0;
+        uint32_t d = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d += ((uint32_t)j < tk.n && (tk.t[j] >> 24) < mi) ? 1u : 0u;
+        ScToks o = tk;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t x = j - nt.n + d;  // old index for slot j >= nt.n
+          const uint32_t ov = x == 0 ? o.t[0] : (x == 1 ? o.t[1] : (x == 2 ? o.t[2] : o.t[3]));
+          tk.t[j] = (uint32_t)j < nt.n ? nt.t[j] : ov;
+        }
+        tk.n = nt.n + o.n - d;
+        P = nP | (P & ~sc_bits(0, mi));
+      }
+    }
+  }
+  STAMP(4)
+
+  // ---- E. the lane's summary, literal runs across lanes, sizes, offsets ----
+  // lead: the first literal run; trail: the last one when the row ends on literals (no copies:
+  // lead == trail); body: every other byte of the lane's output
+  const bool live = s >= c0 && s < ce;
+  uint32_t lead = 0, body = 0, trail = 0;
+  {
+    uint32_t p = s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if ((uint32_t)j < tk.n) {
+        const uint32_t tv = tk.t[j];
+        const uint32_t q = c0 + (tv >> 24), L = (tv >> 16) & 0xffu, run = q - p;
+        if (j == 0)
+          lead = run;
+        else if (run)
+          body += run + 1;  // an internal run (< 16 bytes: a one-byte tag)
+        body += copy_tag_bytes(tv & 0xffffu, L);
+        p = q + L;
+      }
+    }
+    if (live && p < ce) {
+      trail = ce - p;
+      if (tk.n == 0) lead = trail;
+    }
+  }
+  const uint32_t ptrail = __builtin_amdgcn_update_dpp(0u, trail, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane 0: 0)
+  const bool cont = ptrail > 0 && lead > 0;  // this lane's first run continues the previous lane's last one
+  const bool mid = cont && tk.n == 0;         // ... and is all the lane has: the run goes on
+  const uint32_t Cs = scan_dpp(cont ? lead : 0u);
+  uint32_t f = mid ? 64u : lane;  // first lane >= this one where a run stops passing through
+#pragma unroll
+  for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+    const uint32_t o2 = __shfl_down(f, dd, 64);
+    f = lane + dd < 64 ? min(f, o2) : f;
+  }
+  uint32_t fn = __shfl_down(f, 1, 64);
+  fn = (lane == 63 || fn > 63) ? 63u : fn;
+  const uint32_t Cf = __shfl(Cs, fn, 64);
+  const bool starts = trail > 0 && !mid;
+  const uint32_t merged = starts ? trail + Cf - Cs : 0u;  // the run this lane's last run starts
+  uint32_t mts;
+  (void)sc_lit_tag(merged ? merged : 1u, mts);
+  uint32_t size;
+  if (tk.n == 0)
+    size = lead == 0 ? 0u : (cont ? lead : mts + trail);
+  else
+    size = (lead ? (cont ? lead : 1u + lead) : 0u) + body + (trail ? mts + trail : 0u);
+  const uint32_t incl = scan_dpp(size);
+  const uint32_t total = readlane(incl, 63);
+  STAMP(5)
+
+  // ---- G1. the lanes' tokens into the wave's staging buffer (the offset rows: their reads are
+  // done -- the row is in registers) ----
+  uint8_t* const stg = reinterpret_cast<uint8_t*>(Wl.Olo);
+  {
+    const uint32_t stga = lds_addr(stg);
+    uint32_t at = incl - size, p = s;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if ((uint32_t)j < tk.n) {
+        const uint32_t tv = tk.t[j];
+        const uint32_t q = c0 + (tv >> 24), L = (tv >> 16) & 0xffu, off = tv & 0xffffu;
+        const uint32_t run = q - p;  // < 16
+        if (run) {
+          const uint32_t ts = (j == 0 && cont) ? 0u : 1u;
+          sc_lds_put(stga + at, sc_prepend(sc_ld128(S.blk, p), (run - 1) << 2, ts), ts + run);
+          at += ts + run;
+        }
+        if (L <= 64) {
+          uint32_t cs;
+          const uint32_t cv = sc_copy_piece(off, L, cs);
+          sc_lds_put3(stg + at, cv, cs);
+          at += cs;
+        } else {  // emit_copy! (internal.jl:306-329): 64-byte pieces while >= 68, a 60 if > 64, the rest
+          uint32_t R = L;
+          while (R >= 68) {
+            sc_lds_put3(stg + at, (2u + (63u << 2)) | (off << 8), 3);
+            at += 3;
+            R -= 64;
+          }
+          if (R > 64) {
+            sc_lds_put3(stg + at, (2u + (59u << 2)) | (off << 8), 3);
+            at += 3;
+            R -= 60;
+          }
+          uint32_t cs;
+          const uint32_t cv = sc_copy_piece(off, R, cs);
+          sc_lds_put3(stg + at, cv, cs);
+          at += cs;
+        }
+        p = q + L;
+      }
+    }
+    if (live && p < ce) {  // the lane's last run: it starts the merged run, unless it only continues one
+      const uint32_t run = ce - p;
+      uint32_t tag = 0, ts = 0;
+      if (!(tk.n == 0 && cont)) tag = sc_lit_tag(merged, ts);
+      sc_lds_put(stga + at, sc_prepend(sc_ld128(S.blk, p), tag, ts), min(ts + run, 16u));
+      if (ts + run > 16) sc_lds_put(stga + at + 16, sc_ld128(S.blk, p + 16 - ts), ts + run - 16);
+    }
+  }
+  STAMP(6)
+
+  // ---- F. the super-chunk's place in the output ----
+  uint32_t bk;
+  for (uint32_t it = 0; (bk = uniform(__hip_atomic_load(&S.base[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) == 0; ++it) {
+    if (it > kScSpinMax) {
+      S.err = 1;
+      bk = 1;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  if (lane == 0) __hip_atomic_store(&S.base[k + 1], bk + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+
+  // ---- G2. staging -> global: aligned 16-byte stores, bytes at the two partial ends ----
+  {
+    uint8_t* const g = dst + (bk - 1);
+    const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
+    const uint32_t u0 = ad ? 1u : 0u, u1 = (total + ad) >> 4;  // full units [u0, u1); unit u = bytes [16u - ad, +16)
+    uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
+    const uint4* const s16 = reinterpret_cast<const uint4*>(stg);
+    const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;  // a unit starts sb bytes into a staging unit
+    for (uint32_t u = u0 + lane; u < u1; u += 64) {
+      const uint32_t j = 16 * u - ad;  // staging offset of the unit
+      const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
+      const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+      uint32_t r5[5];
+#pragma unroll
+      for (int t = 0; t < 5; ++t) {
+        uint32_t vv = x[t];
+#pragma unroll
+        for (int dd = 1; dd < 4; ++dd) vv = dw == (uint32_t)dd ? x[t + dd] : vv;
+        r5[t] = vv;
+      }
+      g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
+                          __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
+    }
+    const uint32_t nh = min(u0 ? 16 - ad : 0u, total);            // head bytes [0, nh)
+    const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);  // tail bytes [tb, total)
+    const uint32_t nt = total - tb;
+    if (lane < nh + nt) {
+      const uint32_t jj = lane < nh ? lane : tb + (lane - nh);
+      g[jj] = stg[jj];
+    }
+  }
+  STAMP(7)
+  STAMP_FLUSH(g_stamp_sc)
+}
+
 // Persistent: one workgroup per CU walks blocks blockIdx.x, + gridDim.x, ...; each wave loads its
-// share of the next block into registers as soon as its last super-chunk is done, so the HBM
+// share of the next block into registers as soon as it runs out of super-chunks, so the HBM
 // latency of the staging hides behind the block's tail.
 template <int kDummy>
 __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
@@ -251,38 +584,42 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = uniform(tid >> 6);
   const uint32_t lane = tid & 63;
-  STAMP_DECL
-  constexpr int kPf = kBlockSize / 16 / kScThreads;  // 16-byte pieces per thread of a full block
-  uint4 pf[kPf];
-  // block b's length, source, and whether its bytes are in pf (a 16-byte aligned full block)
+  static_assert(kBlockSize / 16 / kScThreads == 4, "four 16-byte pieces per thread of a full block");
+  uint4 pf0, pf1, pf2, pf3;
+  // block b's length, source, and whether its bytes are in pf0..3 (a 16-byte aligned full block)
   uint32_t b = sc_next_block(a, blockIdx.x, lane);
   uint32_t n = 0;
   const uint8_t* src = nullptr;
   bool inpf = false;
-  auto fetch = [&](uint32_t bb) {
-    n = bb < a.nblk ? a.in_len[bb] : 0u;
-    src = bb < a.nblk ? a.in + a.in_off[bb] : nullptr;
-    inpf = bb < a.nblk && n == kBlockSize && ((uintptr_t)src & 15) == 0;
-    if (inpf) {
-      const uint4* s16 = reinterpret_cast<const uint4*>(src);
-#pragma unroll
-      for (int i = 0; i < kPf; ++i) pf[i] = s16[tid + i * kScThreads];
-    }
-  };
-  fetch(b);
+#define SC_FETCH(bb)                                                              \
+  {                                                                               \
+    n = (bb) < a.nblk ? a.in_len[bb] : 0u;                                        \
+    src = (bb) < a.nblk ? a.in + a.in_off[bb] : nullptr;                          \
+    inpf = (bb) < a.nblk && n == kBlockSize && ((uintptr_t)src & 15) == 0;        \
+    if (inpf) {                                                                   \
+      const uint4* s16 = reinterpret_cast<const uint4*>(src);                     \
+      pf0 = s16[tid];                                                             \
+      pf1 = s16[tid + kScThreads];                                                \
+      pf2 = s16[tid + 2 * kScThreads];                                            \
+      pf3 = s16[tid + 3 * kScThreads];                                            \
+    }                                                                             \
+  }
+  SC_FETCH(b)
   while (b < a.nblk) {
     uint8_t* const dst = a.out + a.out_off[b];
     if (n > kBlockSize) {  // (uniform) not a block: error mark, next
       if (tid == 0) a.out_len[b] = 0xffffffffu;
       b = sc_next_block(a, b + gridDim.x, lane);
-      fetch(b);
+      SC_FETCH(b)
       continue;
     }
     // ---- stage the block, clear the table ----
     if (inpf) {
       uint4* d16 = reinterpret_cast<uint4*>(S.blk);
-#pragma unroll
-      for (int i = 0; i < kPf; ++i) d16[tid + i * kScThreads] = pf[i];
+      d16[tid] = pf0;
+      d16[tid + kScThreads] = pf1;
+      d16[tid + 2 * kScThreads] = pf2;
+      d16[tid + 3 * kScThreads] = pf3;
     } else if (((uintptr_t)src & 15) == 0) {
       const uint4* s16 = reinterpret_cast<const uint4*>(src);
       uint4* d16 = reinterpret_cast<uint4*>(S.blk);
@@ -304,282 +641,31 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
       if (lane == 0) {
         S.base[64] = 0;
         S.ins = 0;
+        S.next = 0;
         S.err = 0;
       }
     }
-    // the block after this one (its stride scan now, its bytes when this wave is done)
+    // the block after this one (its stride scan now, its bytes when this wave runs out of work)
     const uint32_t bn = sc_next_block(a, b + gridDim.x, lane);
     __syncthreads();
-    STAMP(8)
 
-  const uint32_t nsc = (n + kScS - 1) / kScS;
-  uint8_t* const Lw = S.L[wave];
-  uint8_t* const Ow = S.O[wave];
-  uint8_t* const Lp = Lw + lane * kScLP;                                       // this lane's slice
-  uint16_t* const Op = reinterpret_cast<uint16_t*>(Ow + lane * kScOP);
-  const uint32_t Tbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)S.T;
-
-  for (uint32_t k = wave; k < nsc; k += kScW) {
-    const uint32_t sc0 = k * kScS, sce = min(sc0 + kScS, n);
-    // ---- A. hashes of the 16 groups: LDS byte address of the bucket, slot value ----
-    uint32_t ha[kScG], hvv[kScG];
-#pragma unroll
-    for (int g = 0; g < (int)kScG; ++g) {
-      const uint32_t q = sc0 + 64 * g + lane;
-      const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, (q & ~3u) + 4), sc_ld32(S.blk, q & ~3u), q & 3u);
-      const uint32_t h = (w * kHashMul) >> (32 - kScTabBits);
-      const bool valid = q + 4 <= n;
-      ha[g] = Tbase + 4 * (valid ? h : (1u << kScTabBits));
-      hvv[g] = (q + 1) << (16 * (g & 1));
-    }
-    const uint32_t mk0 = 0xffffu, mk1 = 0xffff0000u;
-    STAMP(0)
-    STAMP_COUNT(11, 1)
-    // ---- B. the insert token: 16 masked exchanges in position order, then hand it on ----
-    for (uint32_t it = 0; uniform(__hip_atomic_load(&S.ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != k; ++it) {
-      if (it > kScSpinMax) {  // never expected: a broken hand-off must not hang the GPU
-        S.err = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    STAMP(1)
-    __builtin_amdgcn_s_setprio(3);
-    const uint32_t tok_a = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)&S.ins, tok_v = k + 1;
-    uint32_t r[kScG];
-    asm volatile(
-        "ds_mskor_rtn_b32 %0, %16, %32, %34\n"
-        "ds_mskor_rtn_b32 %1, %17, %33, %35\n"
-        "ds_mskor_rtn_b32 %2, %18, %32, %36\n"
-        "ds_mskor_rtn_b32 %3, %19, %33, %37\n"
-        "ds_mskor_rtn_b32 %4, %20, %32, %38\n"
-        "ds_mskor_rtn_b32 %5, %21, %33, %39\n"
-        "ds_mskor_rtn_b32 %6, %22, %32, %40\n"
-        "ds_mskor_rtn_b32 %7, %23, %33, %41\n"
-        "ds_mskor_rtn_b32 %8, %24, %32, %42\n"
-        "ds_mskor_rtn_b32 %9, %25, %33, %43\n"
-        "ds_mskor_rtn_b32 %10, %26, %32, %44\n"
-        "ds_mskor_rtn_b32 %11, %27, %33, %45\n"
-        "ds_mskor_rtn_b32 %12, %28, %32, %46\n"
-        "ds_mskor_rtn_b32 %13, %29, %33, %47\n"
-        "ds_mskor_rtn_b32 %14, %30, %32, %48\n"
-        "ds_mskor_rtn_b32 %15, %31, %33, %49\n"
-        "ds_write_b32 %50, %51\n"
-        "s_waitcnt lgkmcnt(0)"
-        : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
-          "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
-          "=&v"(r[15])
-        : "v"(ha[0]), "v"(ha[1]), "v"(ha[2]), "v"(ha[3]), "v"(ha[4]), "v"(ha[5]), "v"(ha[6]), "v"(ha[7]), "v"(ha[8]),
-          "v"(ha[9]), "v"(ha[10]), "v"(ha[11]), "v"(ha[12]), "v"(ha[13]), "v"(ha[14]), "v"(ha[15]), "v"(mk0), "v"(mk1),
-          "v"(hvv[0]), "v"(hvv[1]), "v"(hvv[2]), "v"(hvv[3]), "v"(hvv[4]), "v"(hvv[5]), "v"(hvv[6]), "v"(hvv[7]),
-          "v"(hvv[8]), "v"(hvv[9]), "v"(hvv[10]), "v"(hvv[11]), "v"(hvv[12]), "v"(hvv[13]), "v"(hvv[14]),
-          "v"(hvv[15]), "v"(tok_a), "v"(tok_v)
-        : "memory");
-    __builtin_amdgcn_s_setprio(0);
-    STAMP(2)
-
-    // ---- C. verify both candidates of every position ----
-#pragma unroll
-    for (int g = 0; g < (int)kScG; ++g) {
-      const uint32_t q = sc0 + 64 * g + lane;
-      const uint32_t sh = 16 * (g & 1);
-      const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
-      const uint32_t c1 = max(ca, cb), c2 = min(ca, cb);
-      const uint32_t avail = q < sce ? sce - q : 0u;  // bytes a match may cover (super-chunk end)
-      const bool ok1 = avail >= 4 && c1 != 0 && c1 - 1 < q, ok2 = avail >= 4 && c2 != 0 && c2 - 1 < q;
-      const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
-      const uint32_t* wq = reinterpret_cast<const uint32_t*>(S.blk + (q & ~3u));
-      const uint32_t* w1 = reinterpret_cast<const uint32_t*>(S.blk + (p1 & ~3u));
-      const uint32_t* w2 = reinterpret_cast<const uint32_t*>(S.blk + (p2 & ~3u));
-      const uint32_t x0 = wq[0], x1 = wq[1], x2 = wq[2];
-      const uint32_t a0 = w1[0], a1 = w1[1], a2 = w1[2];
-      const uint32_t b0 = w2[0], b1 = w2[1], b2 = w2[2];
-      const uint32_t sq = q & 3u, s1 = p1 & 3u, s2 = p2 & 3u;
-      const uint32_t X0 = __builtin_amdgcn_alignbyte(x1, x0, sq), X1 = __builtin_amdgcn_alignbyte(x2, x1, sq);
-      uint32_t l1 = ok1 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(a1, a0, s1), __builtin_amdgcn_alignbyte(a2, a1, s1)) : 0u;
-      uint32_t l2 = ok2 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(b1, b0, s2), __builtin_amdgcn_alignbyte(b2, b1, s2)) : 0u;
-      uint32_t win = 8;
-      // both fill the window: compare the next 8 bytes to choose (the longer match wins)
-      const bool both = l1 == 8 && l2 == 8 && avail > 8;
-      if (ballot(both)) {
-        if (both) {
-          const uint32_t x3 = wq[3], x4 = wq[4], a3 = w1[3], a4 = w1[4], b3 = w2[3], b4 = w2[4];
-          const uint32_t X2 = __builtin_amdgcn_alignbyte(x3, x2, sq), X3 = __builtin_amdgcn_alignbyte(x4, x3, sq);
-          l1 += sc_diff8(X2, X3, __builtin_amdgcn_alignbyte(a3, a2, s1), __builtin_amdgcn_alignbyte(a4, a3, s1));
-          l2 += sc_diff8(X2, X3, __builtin_amdgcn_alignbyte(b3, b2, s2), __builtin_amdgcn_alignbyte(b4, b3, s2));
-          win = 16;
-        }
-      }
-      const bool take2 = l2 > l1;  // ties: the latest (shorter offset)
-      const uint32_t l = take2 ? l2 : l1, c = take2 ? p2 : p1;
-      const uint32_t L = min(l, avail);
-      const bool match = L >= 4;
-      const bool ext = l == win && avail > win;  // the window was full: the walk extends it
-      const uint32_t enc = !match ? 0u : (ext ? win >> 3 : L);
-      const uint32_t pos = 64 * g + lane;  // in the super-chunk: lane slice pos / 16, entry pos % 16
-      Lw[(pos >> 4) * kScLP + (pos & 15)] = (uint8_t)enc;
-      reinterpret_cast<uint16_t*>(Ow + (pos >> 4) * kScOP)[pos & 15] = (uint16_t)(q - c);
-      const uint64_t mb = ballot(match);
-      if (lane == 0) S.M[wave][g] = mb;
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    STAMP(3)
-
-    // ---- D. lane-serial walks, resynchronised ----
-    const uint32_t c0 = sc0 + kScC * lane;
-    const uint32_t ce = c0 < sce ? min(c0 + kScC, sce) : c0;
-    const uint32_t mask16 = reinterpret_cast<const uint16_t*>(S.M[wave])[lane];
-    uint32_t s = c0;
-    ScWalk W = sc_walk(S.blk, Lp, Op, mask16, c0, ce, sce, s);
+    const uint32_t nsc = (n + kScS - 1) / kScS;
     for (;;) {
-      const uint32_t pe = __builtin_amdgcn_update_dpp(0u, W.e, 0x138, 0xf, 0xf, false);  // wave_shr:1
-      const uint32_t sn = lane == 0 ? sc0 : pe;
-      const bool chg = sn != s;
-      if (!ballot(chg)) break;
-      STAMP_COUNT(10, 1)
-      if (chg) s = sn;
-      const ScWalk W2 = sc_walk(S.blk, Lp, Op, mask16, c0, ce, sce, chg ? s : ce);
-      if (chg) W = W2;
+      uint32_t k = 0;
+      if (lane == 0) k = __hip_atomic_fetch_add(&S.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      k = readlane(k, 0);
+      if (k >= nsc) break;
+      sc_superchunk(S, k, n, dst, wave, lane);
     }
-
-    STAMP(4)
-    // ---- E. literal runs across lanes, sizes, offsets ----
-    const uint32_t ptrail = __builtin_amdgcn_update_dpp(0u, W.trail, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane 0: 0)
-    const bool cont = ptrail > 0 && W.lead > 0;  // this lane's first run continues the previous lane's last one
-    const bool mid = cont && W.nc == 0;           // ... and is all the lane has: the run goes on
-    const uint32_t Cs = scan_dpp(cont ? W.lead : 0u);
-    uint32_t f = mid ? 64u : lane;  // first lane >= this one where a run stops passing through
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-      const uint32_t o2 = __shfl_down(f, d, 64);
-      f = lane + d < 64 ? min(f, o2) : f;
+    SC_FETCH(bn)  // the next block's bytes, in flight behind the other waves' last super-chunks
+    __syncthreads();
+    if (wave == 0) {  // this block's result, read before wave 0 re-initialises the hand-off words
+      const uint32_t fin = S.base[nsc], er = S.err;
+      if (lane == 0) a.out_len[b] = er ? 0xffffffffu : fin - 1;
     }
-    uint32_t fn = __shfl_down(f, 1, 64);
-    fn = (lane == 63 || fn > 63) ? 63u : fn;
-    const uint32_t Cf = __shfl(Cs, fn, 64);
-    const bool starts = W.trail > 0 && !mid;
-    const uint32_t merged = starts ? W.trail + Cf - Cs : 0u;  // the run this lane's last run starts
-    uint32_t mts;
-    (void)sc_lit_tag(merged ? merged : 1u, mts);
-    uint32_t size;
-    if (W.nc == 0)
-      size = W.lead == 0 ? 0u : (cont ? W.lead : mts + W.trail);
-    else
-      size = (W.lead ? (cont ? W.lead : 1u + W.lead) : 0u) + W.body + (W.trail ? mts + W.trail : 0u);
-    const uint32_t incl = scan_dpp(size);
-    const uint32_t total = readlane(incl, 63);
-
-    STAMP(5)
-    // ---- G1. the lanes' tokens into the wave's staging buffer (its offset slices: their last
-    // reads are done -- the tokens are in registers) ----
-    uint8_t* const stg = Ow;
-    const uint32_t stga = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)stg;
-    {
-      const bool live = s < ce && s >= c0;
-      uint32_t at = stga + incl - size, p = s;
-      const uint32_t tk[4] = {W.t0, W.t1, W.t2, W.t3};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if ((uint32_t)j < W.nc) {
-          const uint32_t tv = tk[j];
-          const uint32_t q = c0 + (tv >> 24), L = (tv >> 16) & 0xffu, off = tv & 0xffffu;
-          const uint32_t run = q - p;  // < 16
-          if (run) {
-            const bool tagged = !(j == 0 && cont);
-            const uint32_t ts = tagged ? 1u : 0u;
-            sc_lds_put(at, sc_prepend(sc_ld128(S.blk, p), (run - 1) << 2, ts), ts + run);
-            at += ts + run;
-          }
-          if (L <= 64) {
-            uint32_t cs;
-            const uint32_t cv = sc_copy_piece(off, L, cs);
-            sc_lds_put(at, make_uint4(cv, 0, 0, 0), cs);
-            at += cs;
-          } else {  // emit_copy! (internal.jl:306-329): 64-byte pieces while >= 68, a 60 if > 64, the rest
-            uint32_t R = L;
-            while (R >= 68) {
-              sc_lds_put(at, make_uint4((2u + (63u << 2)) | (off << 8), 0, 0, 0), 3);
-              at += 3;
-              R -= 64;
-            }
-            if (R > 64) {
-              sc_lds_put(at, make_uint4((2u + (59u << 2)) | (off << 8), 0, 0, 0), 3);
-              at += 3;
-              R -= 60;
-            }
-            uint32_t cs;
-            const uint32_t cv = sc_copy_piece(off, R, cs);
-            sc_lds_put(at, make_uint4(cv, 0, 0, 0), cs);
-            at += cs;
-          }
-          p = q + L;
-        }
-      }
-      if (live && p < ce) {  // the lane's last run: it starts the merged run, unless it only continues one
-        const uint32_t run = ce - p;
-        uint32_t tag = 0, ts = 0;
-        if (!(W.nc == 0 && cont)) tag = sc_lit_tag(merged, ts);
-        sc_lds_put(at, sc_prepend(sc_ld128(S.blk, p), tag, ts), min(ts + run, 16u));
-        if (ts + run > 16) sc_lds_put(at + 16, sc_ld128(S.blk, p + 16 - ts), ts + run - 16);
-      }
-    }
-    STAMP(6)
-
-    // ---- F. the super-chunk's place in the output ----
-    uint32_t bk;
-    for (uint32_t it = 0; (bk = uniform(__hip_atomic_load(&S.base[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) == 0; ++it) {
-      if (it > kScSpinMax) {
-        S.err = 1;
-        bk = 1;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    if (lane == 0) __hip_atomic_store(&S.base[k + 1], bk + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-
-    // ---- G2. staging -> global: aligned 16-byte stores, bytes at the two partial ends ----
-    {
-      uint8_t* const g = dst + (bk - 1);
-      const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
-      const uint32_t u0 = ad ? 1u : 0u, u1 = (total + ad) >> 4;  // full units [u0, u1); unit u = bytes [16u - ad, +16)
-      uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
-      const uint4* const s16 = reinterpret_cast<const uint4*>(stg);
-      const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;  // a unit starts sb bytes into a staging unit
-      for (uint32_t u = u0 + lane; u < u1; u += 64) {
-        const uint32_t j = 16 * u - ad;  // staging offset of the unit
-        const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
-        const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-        uint32_t r5[5];
-#pragma unroll
-        for (int t = 0; t < 5; ++t) {
-          uint32_t vv = x[t];
-#pragma unroll
-          for (int d = 1; d < 4; ++d) vv = dw == (uint32_t)d ? x[t + d] : vv;
-          r5[t] = vv;
-        }
-        g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
-                            __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
-      }
-      const uint32_t nh = min(u0 ? 16 - ad : 0u, total);           // head bytes [0, nh)
-      const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);  // tail bytes [tb, total)
-      const uint32_t nt = total - tb;
-      if (lane < nh + nt) {
-        const uint32_t jj = lane < nh ? lane : tb + (lane - nh);
-        g[jj] = stg[jj];
-      }
-    }
-    STAMP(7)
+    b = bn;
   }
-  fetch(bn);  // the next block's bytes, in flight behind the other waves' last super-chunks
-  __syncthreads();
-  STAMP(9)
-  if (wave == 0) {  // this block's result, read before wave 0 re-initialises the hand-off words
-    const uint32_t fin = S.base[nsc], er = S.err;
-    if (lane == 0) a.out_len[b] = er ? 0xffffffffu : fin - 1;
-  }
-  b = bn;
-  }
-  STAMP_FLUSH(g_stamp_sc)
+#undef SC_FETCH
 }
 
 #if SM_STAMP

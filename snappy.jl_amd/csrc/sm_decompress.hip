@@ -999,6 +999,11 @@ __device__ inline uint64_t load8z(const uint8_t* __restrict__ in, uint32_t N, ui
   return (uint64_t)load_word(in, N, p) | ((uint64_t)load_word(in, N, p + 4) << 32);
 }
 
+// kFill = false (k_path_check): the same walk without P, recording the reference's exact status
+// of the element's first failing tag (src/internal.jl:499, :505, :518) -- a stream's first error
+// is then the first failing element in path order, found in parallel instead of by the in-order
+// decode.  kErrCross marks an element whose tags do not tile it (the caller falls back).
+template <bool kFill>
 __global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
                                                     const OriginPath* path, uint32_t* __restrict__ P,
                                                     int32_t* status) {
@@ -1022,10 +1027,11 @@ __global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ 
       const uint32_t litlen = (entry & 0xff) + trailer;  // u32 wrap, as the reference
       const uint64_t lsrc = (uint64_t)ip + 1 + taglen;
       if ((c & 3) || lsrc + litlen > N || (uint64_t)op + litlen > size) {  // :518 (a copy here: bad path)
-        st = kErrLiteral;
+        st = (c & 3) ? (kFill ? kErrInvalid : kErrCross) : kErrLiteral;
         break;
       }
-      for (uint32_t i = lane; i < litlen; i += kWave) P[op + i] = 0x80000000u | (uint32_t)(lsrc + i);
+      if (kFill)
+        for (uint32_t i = lane; i < litlen; i += kWave) P[op + i] = 0x80000000u | (uint32_t)(lsrc + i);
       op += litlen;
       ip = (uint32_t)(lsrc + litlen);
       continue;
@@ -1046,23 +1052,27 @@ __global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ 
     const uint32_t incl = scan_dpp(olen);
     const uint32_t opt = op + incl - olen;
     const uint32_t lsrc = tpos + 1 + taglen;
-    const bool bad = mine && (iscopy ? (offset == 0 || offset > opt || (uint64_t)opt + len > size)     // :499, :505
+    const bool bad_off = iscopy && (offset == 0 || offset > opt);                                  // :499
+    const bool bad = mine && (iscopy ? (bad_off || (uint64_t)opt + len > size)                     // :505
                                      : ((uint64_t)lsrc + litlen > N || (uint64_t)opt + litlen > size));  // :518
-    if (ballot(bad)) {
-      st = kErrInvalid;
+    const uint64_t bm = ballot(bad);
+    if (bm) {  // the first failing tag in stream order decides
+      const int32_t code = iscopy ? (bad_off ? kErrCopyOffset : kErrCopyLength) : kErrLiteral;
+      st = kFill ? kErrInvalid : (int32_t)readlane((uint32_t)code, ctz64(bm));
       break;
     }
     // every output byte of the window's tags: tag t's bytes by the whole wave
     for (uint32_t t = 0; t < ntok; ++t) {
       const uint32_t o = readlane(opt, t), L = readlane(olen, t);
       const uint32_t v0 = readlane(iscopy ? 0u - offset : (0x80000000u | lsrc) - o, t);  // P[o+i] = o + i + v0
-      for (uint32_t i = lane; i < L; i += kWave) P[o + i] = o + i + v0;
+      if (kFill)
+        for (uint32_t i = lane; i < L; i += kWave) P[o + i] = o + i + v0;
     }
     op += readlane(incl, ntok - 1);
     ip += readlane(cpos + csz, ntok - 1);
   }
-  if (st == kOk && ip != pe.ex && !(ip >= end && pe.ex >= end)) st = kErrInvalid;  // tags tile the path
-  if (st == kOk && op != pe.O + pe.out) st = kErrInvalid;
+  if (st == kOk && ip != pe.ex && !(ip >= end && pe.ex >= end)) st = kFill ? kErrInvalid : kErrCross;  // tags tile the path
+  if (st == kOk && op != pe.O + pe.out) st = kFill ? kErrInvalid : kErrCross;
   if (lane == 0) status[blockIdx.x] = st;
 }
 
@@ -1088,7 +1098,14 @@ __global__ __launch_bounds__(256) void k_origin_gather(const uint8_t* __restrict
 hipError_t launch_origin_fill(const uint8_t* in, uint32_t N, uint32_t size, const OriginPath* path, uint32_t npath,
                               uint32_t* P, int32_t* status, hipStream_t s) {
   if (npath == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_origin_fill, dim3(npath), dim3(64), 0, s, in, N, size, path, P, status);
+  hipLaunchKernelGGL(k_origin_fill<true>, dim3(npath), dim3(64), 0, s, in, N, size, path, P, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_path_check(const uint8_t* in, uint32_t N, uint32_t size, const OriginPath* path, uint32_t npath,
+                             int32_t* status, hipStream_t s) {
+  if (npath == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_origin_fill<false>, dim3(npath), dim3(64), 0, s, in, N, size, path, nullptr, status);
   return hipGetLastError();
 }
 

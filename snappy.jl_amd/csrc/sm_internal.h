@@ -68,6 +68,10 @@ struct OriginPath {
 };
 hipError_t launch_origin_fill(const uint8_t* in, uint32_t N, uint32_t size, const OriginPath* path, uint32_t npath,
                               uint32_t* P, int32_t* status, hipStream_t s);
+// The same walk without the pointers: per path element, the reference's exact status of its first
+// failing tag (kErrCross: the element's tags do not tile it).
+hipError_t launch_path_check(const uint8_t* in, uint32_t N, uint32_t size, const OriginPath* path, uint32_t npath,
+                             int32_t* status, hipStream_t s);
 hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, hipStream_t s);
 hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)

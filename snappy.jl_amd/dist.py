@@ -117,6 +117,9 @@ def stream_offsets_device(local_sizes, total_len, rank, world, group=None):
     bounds = [shard_range(nfrag, r, world) for r in range(world)]
     m = max(hi - lo for lo, hi in bounds)
     dev = local_sizes.device
+    hl = len(varint32(total_len))
+    if nfrag == 0:  # an empty stream: the header alone
+        return torch.zeros(0, dtype=torch.int64, device=dev), torch.full((1,), hl, dtype=torch.int64, device=dev)
     if world == 1:
         sizes = local_sizes.to(torch.int64)
     else:
@@ -125,7 +128,6 @@ def stream_offsets_device(local_sizes, total_len, rank, world, group=None):
         parts = [torch.empty_like(buf) for _ in range(world)]
         dist.all_gather(parts, buf, group=group)
         sizes = torch.cat([p[: hi - lo] for p, (lo, hi) in zip(parts, bounds)])
-    hl = len(varint32(total_len))
     incl = torch.cumsum(sizes, 0)
     starts = hl + incl - sizes
     lo, hi = bounds[rank]

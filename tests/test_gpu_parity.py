@@ -379,8 +379,8 @@ def test_uncompress_large_stream_parallel(sm, oracle, libsnappy, gpu_available):
 def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
     """Valid streams that are not block-structured (copies into earlier 64 KiB blocks, a
     literal across a fragment start) decode in parallel by origin pointers (path 2) with the
-    oracle's output; corrupted large streams take the in-order decode, with the oracle's
-    status."""
+    oracle's output; corrupted large streams report the oracle's status, their first error
+    found in parallel over the tag path (path 3)."""
     from streams import build, random_ops
     rng = np.random.default_rng(31)
     s1, e1 = build(random_ops(rng, 400_000))                        # offsets up to 65535
@@ -391,6 +391,7 @@ def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
         assert sm.uncompress(s) == e
         assert sm.last_uncompress_path() == 2
     good = oracle.compress(_big_corpus(600_000))
+    paths = []
     for i in range(40):
         bad = bytearray(good)
         for _ in range(int(rng.integers(1, 4))):
@@ -403,6 +404,9 @@ def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
         assert st_g == st_o
         if st_o == 0:
             assert out_g == out_o
+        elif st_o != 18:  # (a broken header never reaches the tag path)
+            paths.append(sm.last_uncompress_path())
+    assert paths and paths.count(3) >= len(paths) // 2, paths  # most errors are found in parallel
 
 
 def _device_batch(streams):
@@ -486,6 +490,38 @@ def test_config5_large_stream(sm, oracle, gpu_available):
     fast = sm.compress(raw, mode="fast")
     assert sm.uncompress(fast) == raw
     assert sm.last_uncompress_path() == 1
+
+
+def test_config5_corrupted_stream_first_error(sm, oracle, gpu_available):
+    """a corrupted config-5 stream (644 MiB, bytes flipped at 10 seeded
+    positions) returns the oracle's status -- the first error in stream order, found by per-tag
+    checks over the tag path in parallel -- in well under half a second (the in-order decode
+    took about a minute)."""
+    import time
+    sys_path_root()
+    import bench
+    raw = bench.large_corpus().tobytes()
+    comp = sm.compress(raw, mode="fast")
+    rng = np.random.default_rng(0xBAD5)
+    hdr = len(sm.encode32(len(raw)))
+    for trial in range(3):
+        bad = bytearray(comp)
+        for pos in rng.integers(hdr, len(bad), 10):
+            bad[int(pos)] ^= int(rng.integers(1, 256))
+        bad = bytes(bad)
+        st_o, _ = oracle.uncompress_status(bad)
+        t0 = time.perf_counter()
+        try:
+            sm.uncompress(bad)
+            st_g = 0
+        except sm.SnappyError as exc:
+            st_g = exc.code
+        dt = time.perf_counter() - t0
+        assert st_g == st_o, (trial, st_g, st_o)
+        if st_o != 0:
+            assert sm.last_uncompress_path() == 3
+            assert dt < 0.5, dt
+        print("trial %d: status %d in %.3f s (path %d)" % (trial, st_g, dt, sm.last_uncompress_path()))
 
 
 def sys_path_root():
