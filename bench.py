@@ -49,7 +49,7 @@ BLOCK = 65536
 SLOT = 76496  # >= max_compressed_length(65536) = 76490, 16-B aligned
 HBM_PEAK_GBPS = 8000.0
 METRIC = "GB/s compressed+decompressed (batched blocks) at 1/2/4/8 GPUs; % HBM peak"  # BASELINE.json
-ROUND = "r02"
+ROUND = "r03"
 
 # test/runtests.jl:8-24, the round-trip corpus; config 5 tiles it
 ROUNDTRIP_FILES = ["alice29.txt", "asyoulik.txt", "html", "html_x_4", "kppkn.gtb", "lcet10.txt", "fireworks.jpeg",
@@ -109,11 +109,35 @@ def random_blocks(nblk, seed):
 
 # ---- launching ranks ----------------------------------------------------------------------
 
+def visible_gpus():
+    """GPUs this process may use, without touching the GPU runtime: the KFD topology in sysfs
+    (nodes with a GPU id), narrowed by HIP/ROCR/CUDA_VISIBLE_DEVICES when set."""
+    n = 0
+    root = "/sys/class/kfd/kfd/topology/nodes"
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "gpu_id")) as fh:
+                    n += int(fh.read().strip() or "0") != 0
+            except (OSError, ValueError):
+                pass
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(args):
-    """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run (this process
-    has not touched the GPU; torch.cuda.device_count() does not initialise it on this image)."""
-    import torch
-    ndev = torch.cuda.device_count()
+    """--gpus N > 1 without a launcher: start N ranks under torch.distributed.run.  The GPUs are
+    counted from sysfs, and the script refuses to spawn from a process that has initialised the
+    GPU runtime (a child must not inherit it)."""
+    if "torch" in sys.modules and sys.modules["torch"].cuda.is_initialized():
+        print("bench.py: the GPU runtime is already initialised; refusing to start ranks", file=sys.stderr)
+        return 2
+    ndev = visible_gpus()
     if ndev < args.gpus:
         print("bench.py: --gpus %d but only %d GPU(s) visible" % (args.gpus, ndev), file=sys.stderr)
         return 2
@@ -510,6 +534,7 @@ def main():
         batch.uncompress(sm)
 
     elapsed = timed_steps(step, args.steps, args.warmup, world, dist, dev)
+    headline_sizes = batch.comp_len.clone()
     comp_bytes = batch.comp_bytes()
     in_bytes = batch.in_bytes
     t_c = kernel_ms(lambda: batch.compress(sm), reps)
@@ -614,10 +639,18 @@ def main():
         extras["config5_host_stream"] = config5_host_stream(sm, big)
         ok_all &= extras["config5_host_stream"]["ok"]
 
+    rccl = None
     if use_dist:
         t = torch.tensor([0 if ok_all else 1], dtype=torch.int32, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ok_all = int(t.item()) == 0
+        # what the communicator saw: its backend and size, and the gathered size table (every
+        # rank's u32 compressed sizes; this rank's own slice must equal its local sizes)
+        own = sizes_all[rank * args.blocks:(rank + 1) * args.blocks]
+        rccl = {"backend": str(dist.get_backend()), "world": dist.get_world_size(),
+                "sizes_gathered": int(sizes_all.numel()),
+                "own_slice_matches": bool(torch.equal(own, headline_sizes))}
+        ok_all &= rccl["own_slice_matches"]
 
     cpu = None
     if rank == 0 and not args.no_cpu:
@@ -651,6 +684,7 @@ def main():
             "all_roundtrips_bit_exact": ok_all,
             "roofline": roofline(dom, kern[dom][1], kern[dom][0]),
             "roofline_other": roofline(*[(k, v[1], v[0]) for k, v in kern.items() if k != dom][0]),
+            "rccl": rccl,
             "random": rnd,
             "large": large,
             "reference_mode": ref_mode,

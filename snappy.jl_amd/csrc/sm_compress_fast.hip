@@ -795,26 +795,59 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 
 
 // ---- incompressible screen ---------------------------------------------------------------
-// Before the parse, one light workgroup per block samples kScrWin windows of kScrWB bytes spread
-// evenly over the block and counts the sample positions whose 4 bytes occurred earlier in the
-// sample.  Compressible data counts in the thousands (text 900-1700 of the 4,000 positions,
-// structured data 2,000-3,400); compressed, encrypted and random data counts 0-130 (jpeg,
-// the tail of a pdf, a snappy stream).  Below kScrMin the block is emitted here as ONE literal
-// (header, emit_literal! tag, the bytes: internal.jl:271-284 -- the reference's own output for
-// random 64 KiB blocks is also one 65,542-B literal), copied with aligned 16-B loads and stores
-// at HBM speed; the parse kernel then skips it.  This is the batch analogue of the reference's
-// skip heuristic (internal.jl:162-175), which stops looking for matches in data without them.
-// The bet only costs ratio, never validity: a literal encodes any bytes.
-constexpr uint32_t kScrWin = 32, kScrWB = 128;  // 4 KiB sample
-constexpr uint32_t kScrMin = 192;               // repeated sample positions that make a block "compressible"
-constexpr uint32_t kScrMinLen = 8192;           // smaller blocks always take the parse
-constexpr uint32_t kScrThreads = 256;
+// Before the parse, one light workgroup per block looks for repeated content anywhere in the block
+// through content-defined anchors: the positions whose 4-byte word hashes into the top 1/64 of the
+// hash range (the reference's multiply, internal.jl:94).  Repeated content repeats its anchors at
+// any distance, so a block counts the anchors whose word an earlier-inserted anchor already had
+// (an LDS table of 4 K words, exchanged).  Text and structured data count hundreds; random,
+// compressed and encrypted data count ~0.  The first 16 KiB go first (text decides there); the rest
+// of the block is read only when they show no repeats.  Below kScrMin the block is emitted here as
+// ONE literal (header, emit_literal! tag, the bytes: internal.jl:271-284 -- the reference's own
+// output for random 64 KiB blocks is also one 65,542-B literal) from the registers that read it,
+// with aligned 16-B stores: an incompressible block is read once and written once.  The parse
+// kernel then skips it.  This is the batch analogue of the reference's skip heuristic
+// (internal.jl:162-175).  The bet only costs ratio, never validity: a literal encodes any bytes,
+// and a block with fewer than kScrMin repeated anchors has ~kScrMin x 64 B of repeats at most.
+constexpr uint32_t kScrMin = 8;           // repeated anchors that make a block "compressible"
+constexpr uint32_t kScrMinLen = 8192;     // smaller blocks always take the parse
+constexpr uint32_t kScrThreads = 512;
+constexpr uint32_t kScrPieces = kBlockSize / 16 / kScrThreads;  // 16-B pieces per thread (8)
+constexpr uint32_t kScrFirst = 2;                               // pieces of the first pass (16 KiB)
 constexpr uint32_t kScrTabBits = 12;
+constexpr uint32_t kScrEmpty = 0xffffffffu;  // its hash is no anchor, so no anchor word equals it
+static_assert(((kScrEmpty * kHashMul) >> 26) != 0, "the empty mark must not be an anchor word");
+
+// 16 bytes of src at o (any alignment of src), zero past n
+__device__ inline uint4 scr_load16(const uint8_t* src, uint32_t o, uint32_t n, bool aligned) {
+  if (aligned && o + 16 <= n) return *reinterpret_cast<const uint4*>(src + o);
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (uint32_t k = 0; k < 16; ++k)
+    if (o + k < n) w[k >> 2] |= (uint32_t)src[o + k] << (8 * (k & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// repeated anchors among the 16 positions of a piece v (bytes [o, o + 16)), nv = the next piece
+// (valid = its first 3 bytes are real: the positions 13..15 have their 4 bytes)
+__device__ inline uint32_t scr_anchors(uint32_t* tab, uint4 v, uint4 nv, uint32_t o, uint32_t n, bool nvalid) {
+  const uint32_t x[5] = {v.x, v.y, v.z, v.w, nv.x};
+  uint32_t rep = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j) {
+    const uint32_t w = (j & 3) ? __builtin_amdgcn_alignbyte(x[(j >> 2) + 1], x[j >> 2], j & 3) : x[j >> 2];
+    const uint32_t h = w * kHashMul;
+    const bool ok = o + j + 4 <= n && (j < 13 || nvalid);
+    if (ok && (h >> 26) == 0) {
+      const uint32_t old = atomicExch(&tab[(h >> 14) & ((1u << kScrTabBits) - 1)], w);
+      rep += old == w ? 1u : 0u;
+    }
+  }
+  return rep;
+}
 
 __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t samp[kScrWin * kScrWB + 16];
   __shared__ uint32_t tab[1u << kScrTabBits];
-  __shared__ uint32_t cnt;
+  __shared__ uint32_t cnt[2];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t b = blockIdx.x;
   const uint32_t n = a.in_len[b];
@@ -824,116 +857,91 @@ __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) 
     if (tid == 0) a.out_len[b] = kScreenTodo;
     return;
   }
-  // (1) the sample: window i at (i (n - WB) / (W - 1)) & ~15, one 16-B piece per thread
-  static_assert(kScrWin * kScrWB == 16 * kScrThreads, "one piece per thread");
-  {
-    const uint32_t w = tid / (kScrWB / 16), k = tid % (kScrWB / 16);
-    const uint32_t o = ((w * (n - kScrWB)) / (kScrWin - 1)) & ~15u;
-    const uint8_t* s = src + o + 16 * k;
-    uint4 v;
-    if (((uintptr_t)src & 15) == 0) {
-      v = *reinterpret_cast<const uint4*>(s);
-    } else {
-      uint32_t x[4];
+  const bool aligned = ((uintptr_t)src & 15) == 0;
+  for (uint32_t k = tid; k < (1u << kScrTabBits); k += kScrThreads) tab[k] = kScrEmpty;
+  if (tid < 2) cnt[tid] = 0;
+  uint4 v[kScrPieces];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        x[i] = (uint32_t)s[4 * i] | ((uint32_t)s[4 * i + 1] << 8) | ((uint32_t)s[4 * i + 2] << 16) |
-               ((uint32_t)s[4 * i + 3] << 24);
-      v = make_uint4(x[0], x[1], x[2], x[3]);
+  for (uint32_t i = 0; i < kScrPieces; ++i) v[i] = make_uint4(0, 0, 0, 0);
+  // piece i of thread t: bytes [16 (t + 512 i), +16); lane + 1 holds the next piece (a wave's last
+  // lane: its positions 13..15 are skipped -- 3 of every 1,024)
+  auto pass = [&](uint32_t i0, uint32_t i1, uint32_t slot) {
+#pragma unroll
+    for (uint32_t i = i0; i < i1; ++i) v[i] = scr_load16(src, 16 * (tid + kScrThreads * i), n, aligned);
+    __syncthreads();  // (the table is initialised)
+    uint32_t rep = 0;
+#pragma unroll
+    for (uint32_t i = i0; i < i1; ++i) {
+      uint4 nv;
+      nv.x = __builtin_amdgcn_update_dpp(0u, v[i].x, 0x130, 0xf, 0xf, false);  // wave_shl:1
+      rep += scr_anchors(tab, v[i], nv, 16 * (tid + kScrThreads * i), n, lane < 63);
     }
-    reinterpret_cast<uint4*>(samp)[tid] = v;
-  }
-  for (uint32_t k = tid; k < (1u << kScrTabBits); k += kScrThreads) tab[k] = 0xffffffffu;
-  if (tid == 0) cnt = 0;
-  if (tid < 4) reinterpret_cast<uint32_t*>(samp + kScrWin * kScrWB)[tid] = 0;
-  __syncthreads();
-  // (2) first occurrence of every sample 4-gram (atomic min), then the repeats
-  constexpr uint32_t kPer = kScrWin * kScrWB / kScrThreads;  // 16 positions per thread, strided by 256
-  uint32_t wv[kPer], hv[kPer];
-#pragma unroll
-  for (uint32_t i = 0; i < kPer; ++i) {
-    const uint32_t p = tid + kScrThreads * i;
-    wv[i] = lds_ld32(samp, p);
-    hv[i] = (wv[i] * kHashMul) >> (32 - kScrTabBits);
-    if (p % kScrWB <= kScrWB - 4) atomicMin(&tab[hv[i]], p);
-  }
-  __syncthreads();
-  uint32_t mine = 0;
-#pragma unroll
-  for (uint32_t i = 0; i < kPer; ++i) {
-    const uint32_t p = tid + kScrThreads * i;
-    const uint32_t q = tab[hv[i]];
-    mine += (p % kScrWB <= kScrWB - 4 && q < p && lds_ld32(samp, q) == wv[i]) ? 1u : 0u;
-  }
-  const uint32_t wsum = __builtin_amdgcn_readlane(scan_dpp(mine), 63);
-  if (lane == 0) atomicAdd(&cnt, wsum);
-  __syncthreads();
-  if (cnt >= kScrMin) {
+    rep = __builtin_amdgcn_readlane(scan_dpp(rep), 63);
+    if (lane == 0 && rep) atomicAdd(&cnt[slot], rep);
+    __syncthreads();
+  };
+  pass(0, kScrFirst, 0);
+  if (cnt[0] >= kScrMin) {  // text and structured data decide on their first 16 KiB
     if (tid == 0) a.out_len[b] = kScreenTodo;
     return;
   }
-  // (3) literal-only stream: [varint n] + literal tag + the n bytes.  D[j] = src[j - h] for
-  // j >= h.  Destination 16-B units that lie inside [h, h + n) are assembled from two aligned
-  // source units (the second from the neighbouring lane, DPP) with one byte shift; the partial
+  if (n > 16 * kScrThreads * kScrFirst) pass(kScrFirst, kScrPieces, 1);
+  if (cnt[0] + cnt[1] >= kScrMin) {
+    if (tid == 0) a.out_len[b] = kScreenTodo;
+    return;
+  }
+  // literal-only stream from the registers: D[j] = src[j - h] for j >= h.  Piece p (source bytes
+  // [16p, 16p + 16)) makes the aligned output unit that starts m bytes into it, m = -(ad + h) mod
+  // 16, from its bytes and the next piece's (lane + 1; a wave's last lane reloads it).  The partial
   // units at either end are written byte by byte.
   const uint32_t hv0 = a.header ? varint_len(n) : 0u;
   const uint32_t h = hv0 + literal_tag_bytes(n);
-  const uint32_t ad = (uint32_t)((uintptr_t)dst & 15), as = (uint32_t)((uintptr_t)src & 15);
-  // dst unit u covers D offsets [16u - ad, 16u - ad + 16); the source of its first byte is
-  // src-aligned offset 16u + e, e = as - ad - h
-  const int32_t e = (int32_t)as - (int32_t)ad - (int32_t)h;
-  const int32_t E = e >= 0 ? e / 16 : -((15 - e) / 16);  // floor(e / 16)
-  const uint32_t m = (uint32_t)(e - 16 * E);              // byte shift 0..15
-  const uint32_t u0 = (h + ad + 15) / 16;                 // first full unit
-  const uint32_t u1 = (h + n + ad) / 16;                  // one past the last full unit
-  const uint4* s16 = reinterpret_cast<const uint4*>(src - as);
+  const uint32_t ad = (uint32_t)((uintptr_t)dst & 15);
+  const uint32_t m = (16u - ((ad + h) & 15u)) & 15u;
   uint4* d16 = reinterpret_cast<uint4*>(dst - ad);
-  const uint32_t send = as + n;  // src-aligned byte offset one past the block
-  for (uint32_t base = u0 + (tid & ~63u); base < u1; base += kScrThreads) {
-    const uint32_t u = base + lane;
-    const int32_t su = (int32_t)u + E;  // >= 0 for full units
-    uint4 lo = make_uint4(0, 0, 0, 0), hi;
-    if (u < u1) lo = s16[su];
-    // the next source unit: the next lane's lo, except in lane 63 and past u1
-    hi.x = __builtin_amdgcn_update_dpp(0u, lo.x, 0x130, 0xf, 0xf, false);
-    hi.y = __builtin_amdgcn_update_dpp(0u, lo.y, 0x130, 0xf, 0xf, false);
-    hi.z = __builtin_amdgcn_update_dpp(0u, lo.z, 0x130, 0xf, 0xf, false);
-    hi.w = __builtin_amdgcn_update_dpp(0u, lo.w, 0x130, 0xf, 0xf, false);
-    if ((lane == 63 || u + 1 >= u1) && u < u1 && m != 0 && 16u * (uint32_t)(su + 1) < send) hi = s16[su + 1];
-    if (u < u1) {
-      const uint32_t x[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-      const uint32_t dw = m >> 2, sb = m & 3u;
+  const uint32_t u_of_p0 = (m + ad + h) >> 4;  // the unit of piece 0
+  const uint32_t dw = m >> 2, bs = m & 3u;
+#pragma unroll
+  for (uint32_t i = 0; i < kScrPieces; ++i) {
+    const uint32_t p = tid + kScrThreads * i;
+    const bool full = 16 * p + m + 16 <= n;
+    uint4 nv;
+    nv.x = __builtin_amdgcn_update_dpp(0u, v[i].x, 0x130, 0xf, 0xf, false);
+    nv.y = __builtin_amdgcn_update_dpp(0u, v[i].y, 0x130, 0xf, 0xf, false);
+    nv.z = __builtin_amdgcn_update_dpp(0u, v[i].z, 0x130, 0xf, 0xf, false);
+    nv.w = __builtin_amdgcn_update_dpp(0u, v[i].w, 0x130, 0xf, 0xf, false);
+    if (lane == 63 && full && m != 0) nv = scr_load16(src, 16 * (p + 1), n, aligned);
+    if (full) {
+      const uint32_t x[8] = {v[i].x, v[i].y, v[i].z, v[i].w, nv.x, nv.y, nv.z, nv.w};
       uint32_t r[5];
 #pragma unroll
       for (int k = 0; k < 5; ++k) {  // x[dw + k], selects (no dynamic register indexing)
-        uint32_t v = x[k];
+        uint32_t t = x[k];
 #pragma unroll
-        for (int d = 1; d < 4; ++d) v = dw == (uint32_t)d ? x[k + d] : v;
-        r[k] = v;
+        for (int d = 1; d < 4; ++d) t = dw == (uint32_t)d ? x[k + d] : t;
+        r[k] = t;
       }
-      uint4 o;
-      o.x = __builtin_amdgcn_alignbyte(r[1], r[0], sb);
-      o.y = __builtin_amdgcn_alignbyte(r[2], r[1], sb);
-      o.z = __builtin_amdgcn_alignbyte(r[3], r[2], sb);
-      o.w = __builtin_amdgcn_alignbyte(r[4], r[3], sb);
-      d16[u] = o;
+      d16[u_of_p0 + p] = make_uint4(__builtin_amdgcn_alignbyte(r[1], r[0], bs), __builtin_amdgcn_alignbyte(r[2], r[1], bs),
+                                    __builtin_amdgcn_alignbyte(r[3], r[2], bs), __builtin_amdgcn_alignbyte(r[4], r[3], bs));
     }
   }
-  // partial units: D offsets [0, 16 u0 - ad) and [16 u1 - ad, h + n), plus the header bytes
-  const uint32_t headEnd = min(16 * u0 - ad, h + n), tailBeg = max(16 * u1 - ad, headEnd);
+  // the head: header + source bytes [0, m); the tail: source bytes past the last full unit
+  const uint32_t nfull = n >= m + 16 ? (n - m) / 16 : 0u;
+  const uint32_t headEnd = h + min(m, n);             // D bytes [0, headEnd)
+  const uint32_t tailBeg = nfull ? h + m + 16 * nfull : headEnd;  // D bytes [tailBeg, h + n)
   const uint32_t nh = headEnd, nt = h + n - tailBeg;
   for (uint32_t j = tid; j < nh + nt; j += kScrThreads) {
     const uint32_t jj = j < nh ? j : tailBeg + (j - nh);
-    uint8_t v;
+    uint8_t c;
     if (jj < hv0) {
-      v = (uint8_t)(((n >> (7 * jj)) & 0x7f) | (jj + 1 < hv0 ? 0x80 : 0));
+      c = (uint8_t)(((n >> (7 * jj)) & 0x7f) | (jj + 1 < hv0 ? 0x80 : 0));
     } else if (jj < h) {  // emit_literal! tag: 60..63 << 2 then len-1 little-endian
       const uint32_t tb = h - hv0, k = jj - hv0;
-      v = tb == 1 ? (uint8_t)((n - 1) << 2) : (k == 0 ? (uint8_t)((58 + tb) << 2) : (uint8_t)((n - 1) >> (8 * (k - 1))));
+      c = tb == 1 ? (uint8_t)((n - 1) << 2) : (k == 0 ? (uint8_t)((58 + tb) << 2) : (uint8_t)((n - 1) >> (8 * (k - 1))));
     } else {
-      v = src[jj - h];
+      c = src[jj - h];
     }
-    dst[jj] = v;
+    dst[jj] = c;
   }
   if (tid == 0) a.out_len[b] = h + n;
 }

@@ -41,13 +41,25 @@ constexpr uint32_t kScreenTodoSc = 0xfffffffeu;  // k_literal_screen's "parse th
 constexpr uint32_t kScS = 1024;           // super-chunk bytes
 constexpr uint32_t kScC = kScS / 64;      // positions per lane (16)
 constexpr uint32_t kScG = kScS / 64;      // 64-position groups per super-chunk (16)
-constexpr uint32_t kScW = 16;             // waves per workgroup
+constexpr uint32_t kScW = 16;             // waves per workgroup: kScW - 1 workers and the writer
+constexpr uint32_t kScWorkers = kScW - 1;
+constexpr uint32_t kScRing = 8;           // staging slots between the workers and the writer
+constexpr uint32_t kScSlot = 1280;        // bytes per slot (a super-chunk's output is at most ~1.1 KiB)
 constexpr uint32_t kScThreads = 64 * kScW;
 constexpr uint32_t kScTabBits = 13;       // 8 K dwords = 16 K u16 slots
 constexpr uint32_t kScMaxL = 255;         // longest copy token (u8 lengths)
-constexpr uint32_t kScMaxSc = kBlockSize / kScS;
-constexpr uint32_t kScSpinMax = 1u << 22;  // hand-off polls (64 cycles each) before a wait gives up
+#ifndef SC_SPIN_BITS
+#define SC_SPIN_BITS 22
+#endif
+constexpr uint32_t kScSpinMax = 1u << SC_SPIN_BITS;  // hand-off polls (64+ cycles each) before a wait gives up
 static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, one 16-byte row");
+
+// Diagnostic builds only (-DSC_ABL=bits, tools/sc_abl.py): 1 no emission (G1, G2), 2 no resync
+// (first walks only), 4 no 16-byte choice between two full candidates, 8 no candidates (the
+// verify reads nothing), 16 no insert-token wait, 32 no base wait.  The output is not valid.
+#ifndef SC_ABL
+#define SC_ABL 0
+#endif
 
 #if SM_STAMP
 __device__ unsigned long long g_stamp_sc[12];
@@ -58,20 +70,37 @@ STAMP_MACROS(12)
 struct ScWaveLds {
   uint8_t L[kScS];         // match length byte per position (0: none; 1/2: extend from 8/16)
   uint16_t Olo[kScS / 2];  // offsets of positions 0..7 of each row
-  uint16_t Ohi[kScS / 2];  // offsets of positions 8..15 of each row (Olo + Ohi: the staging buffer later)
+  uint16_t Ohi[kScS / 2];  // offsets of positions 8..15 of each row
 };
 struct ScLds {
   uint8_t blk[kBlockSize + 64];        // the block (+ pad: reads run up to 20 bytes past a position)
   uint32_t T[(1u << kScTabBits) + 4];  // hash table; T[1 << kScTabBits] is the dummy for invalid lanes
-  ScWaveLds w[kScW];
-  uint64_t M[kScW][kScG];              // per wave: match bitmask (bit = position of the super-chunk)
+  ScWaveLds w[kScWorkers];
+  uint8_t ring[kScRing][kScSlot];      // staged outputs: super-chunk k in slot k % kScRing
+  uint64_t M[kScWorkers][kScG];        // per worker: match bitmask (bit = position of the super-chunk)
+  uint32_t rsize[kScRing];             // the staged super-chunk's output size + 1 (0: slot not staged)
+  uint32_t rseq[kScRing];              // the super-chunk a slot takes next (the writer frees it so)
   uint32_t ins;                        // insert token: super-chunks inserted so far
   uint32_t next;                       // the next super-chunk to take
   uint32_t err;                        // a hand-off wait timed out (never expected)
-  uint32_t base[kScMaxSc + 1];         // output offset of super-chunk k, + 1 (0: not known yet)
 };
 static_assert(sizeof(ScLds) <= 160 * 1024, "LDS");
 static_assert(sizeof(ScWaveLds) % 16 == 0 && offsetof(ScLds, w) % 16 == 0, "rows are 16-byte aligned");
+static_assert(kScSlot % 16 == 0 && offsetof(ScLds, ring) % 16 == 0, "slots are 16-byte aligned");
+
+// wait (bounded) until the LDS word at p satisfies pred; false if the wait gave up
+template <typename Pred>
+__device__ __attribute__((always_inline)) inline uint32_t sc_wait(uint32_t* p, Pred pred, uint32_t& err, uint32_t code) {
+  uint32_t v;
+  for (uint32_t it = 0; !pred(v = uniform(__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP))); ++it) {
+    if (it > kScSpinMax) {  // never expected: a broken hand-off must not hang the GPU
+      err |= code;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return v;
+}
 
 __device__ inline uint32_t sc_ld32(const uint8_t* blk, uint32_t a) { return *reinterpret_cast<const uint32_t*>(blk + a); }
 
@@ -187,8 +216,8 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_next_block(const Co
 }
 
 // One super-chunk, by one wave (sections A-G2 above).
-__device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, const uint32_t k, const uint32_t n, uint8_t* const dst,
-                                     const uint32_t wave, const uint32_t lane) {
+__device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, const uint32_t k, const uint32_t n,
+                                                                   const uint32_t wave, const uint32_t lane) {
   ScWaveLds& Wl = S.w[wave];
   const uint32_t sc0 = k * kScS, sce = min(sc0 + kScS, n);
   const uint32_t Tbase = lds_addr(S.T);
@@ -208,9 +237,9 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   STAMP(0)
   STAMP_COUNT(11, 1)
   // ---- B. the insert token: 16 masked exchanges in position order, then hand it on ----
-  for (uint32_t it = 0; uniform(__hip_atomic_load(&S.ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != k; ++it) {
+  for (uint32_t it = 0; !(SC_ABL & 16) && uniform(__hip_atomic_load(&S.ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != k; ++it) {
     if (it > kScSpinMax) {  // never expected: a broken hand-off must not hang the GPU
-      S.err = 1;
+      S.err |= 1;  // (the insert token)
       break;
     }
     __builtin_amdgcn_s_sleep(1);
@@ -255,7 +284,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t q = sc0 + 64 * g + lane;
     const uint32_t sh = 16 * (g & 1);
     const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
-    const uint32_t c1 = max(ca, cb), c2 = min(ca, cb);
+    const uint32_t c1 = (SC_ABL & 8) ? 0u : max(ca, cb), c2 = (SC_ABL & 8) ? 0u : min(ca, cb);
     const uint32_t avail = q < sce ? sce - q : 0u;  // bytes a match may cover (super-chunk end)
     // (c - 1 < q also rejects c == 0; only invalid lanes -- avail < 4 -- can see other values)
     const bool ok1 = avail >= 4 && c1 - 1 < q, ok2 = avail >= 4 && c2 - 1 < q;
@@ -272,7 +301,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     uint32_t l2 = ok2 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(b1, b0, s2), __builtin_amdgcn_alignbyte(b2, b1, s2)) : 0u;
     uint32_t win = 8;
     // both fill the window: compare the next 8 bytes to choose (the longer match wins)
-    const bool both = l1 == 8 && l2 == 8 && avail > 8;
+    const bool both = !(SC_ABL & 4) && l1 == 8 && l2 == 8 && avail > 8;
     if (ballot(both)) {
       if (both) {
         const uint32_t x3 = wq[3], x4 = wq[4], a3 = w1[3], a4 = w1[4], b3 = w2[3], b4 = w2[4];
@@ -385,7 +414,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       e = c0;
     }
   }
-  for (;;) {
+  for (; !(SC_ABL & 2);) {
     const uint32_t pe = __builtin_amdgcn_update_dpp(0u, e, 0x138, 0xf, 0xf, false);  // wave_shr:1
     const uint32_t sn = lane == 0 ? sc0 : pe;
     const bool chg = sn != s;
@@ -476,10 +505,15 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   const uint32_t total = readlane(incl, 63);
   STAMP(5)
 
-  // ---- G1. the lanes' tokens into the wave's staging buffer (the offset rows: their reads are
-  // done -- the row is in registers) ----
-  uint8_t* const stg = reinterpret_cast<uint8_t*>(Wl.Olo);
-  {
+  // ---- F. a staging slot: super-chunk k takes slot k % kScRing once the writer has written
+  // super-chunk k - kScRing out of it ----
+  const uint32_t slot = k % kScRing;
+  (void)sc_wait(&S.rseq[slot], [&](uint32_t v) { return v == k; }, S.err, 2u);
+  STAMP(6)
+
+  // ---- G. the lanes' tokens into the slot, then the slot to the writer ----
+  uint8_t* const stg = S.ring[slot];
+  if (!(SC_ABL & 1)) {
     const uint32_t stga = lds_addr(stg);
     uint32_t at = incl - size, p = s;
 #pragma unroll
@@ -526,53 +560,88 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       if (ts + run > 16) sc_lds_put(stga + at + 16, sc_ld128(S.blk, p + 16 - ts), ts + run - 16);
     }
   }
-  STAMP(6)
-
-  // ---- F. the super-chunk's place in the output ----
-  uint32_t bk;
-  for (uint32_t it = 0; (bk = uniform(__hip_atomic_load(&S.base[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) == 0; ++it) {
-    if (it > kScSpinMax) {
-      S.err = 1;
-      bk = 1;
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  if (lane == 0) __hip_atomic_store(&S.base[k + 1], bk + total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-
-  // ---- G2. staging -> global: aligned 16-byte stores, bytes at the two partial ends ----
-  {
-    uint8_t* const g = dst + (bk - 1);
-    const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
-    const uint32_t u0 = ad ? 1u : 0u, u1 = (total + ad) >> 4;  // full units [u0, u1); unit u = bytes [16u - ad, +16)
-    uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
-    const uint4* const s16 = reinterpret_cast<const uint4*>(stg);
-    const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;  // a unit starts sb bytes into a staging unit
-    for (uint32_t u = u0 + lane; u < u1; u += 64) {
-      const uint32_t j = 16 * u - ad;  // staging offset of the unit
-      const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
-      const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-      uint32_t r5[5];
-#pragma unroll
-      for (int t = 0; t < 5; ++t) {
-        uint32_t vv = x[t];
-#pragma unroll
-        for (int dd = 1; dd < 4; ++dd) vv = dw == (uint32_t)dd ? x[t + dd] : vv;
-        r5[t] = vv;
-      }
-      g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
-                          __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
-    }
-    const uint32_t nh = min(u0 ? 16 - ad : 0u, total);            // head bytes [0, nh)
-    const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);  // tail bytes [tb, total)
-    const uint32_t nt = total - tb;
-    if (lane < nh + nt) {
-      const uint32_t jj = lane < nh ? lane : tb + (lane - nh);
-      g[jj] = stg[jj];
-    }
-  }
+  // (a wave's LDS operations execute in order: the writer that sees the size sees the bytes)
+  __hip_atomic_store(&S.rsize[slot], total + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // (all lanes: same value)
   STAMP(7)
   STAMP_FLUSH(g_stamp_sc)
+}
+
+// the staged bytes [0, len) of an LDS buffer (16-byte aligned) to global g (any alignment): aligned
+// 16-byte stores of byte-shifted units, bytes at the two partial ends (one wave)
+__device__ __attribute__((always_inline)) inline void sc_copy_out(uint8_t* const g, const uint8_t* stg, uint32_t len,
+                                                                 uint32_t lane) {
+  const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
+  const uint32_t u0 = ad ? 1u : 0u, u1 = (len + ad) >> 4;  // full units [u0, u1); unit u = bytes [16u - ad, +16)
+  uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
+  const uint4* const s16 = reinterpret_cast<const uint4*>(stg);
+  const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;  // a unit starts sb bytes into a staging unit
+  for (uint32_t u = u0 + lane; u < u1; u += 64) {
+    const uint32_t j = 16 * u - ad;  // staging offset of the unit
+    const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
+    const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    uint32_t r5[5];
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      uint32_t vv = x[t];
+#pragma unroll
+      for (int dd = 1; dd < 4; ++dd) vv = dw == (uint32_t)dd ? x[t + dd] : vv;
+      r5[t] = vv;
+    }
+    g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
+                        __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
+  }
+  const uint32_t nh = min(u0 ? 16 - ad : 0u, len);              // head bytes [0, nh)
+  const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);  // tail bytes [tb, len)
+  const uint32_t nt = len - tb;
+  if (lane < nh + nt) {
+    const uint32_t jj = lane < nh ? lane : tb + (lane - nh);
+    g[jj] = stg[jj];
+  }
+}
+
+// The writer wave: the staged super-chunks in order, each at the running output offset (no wave
+// waits for another's offset), then the block's length.  A block whose parse came out larger than
+// one literal of the whole block (a nearly incompressible block past the screen) is rewritten as
+// that literal (emit_literal!, internal.jl:271-284): the output never exceeds the literal size.
+__device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, const CompressArgs& a, uint32_t b, uint32_t n,
+                                                               uint8_t* const dst, uint32_t hv, uint32_t nsc,
+                                                               uint32_t lane) {
+  uint32_t o = hv, err = 0;
+  for (uint32_t k = 0; k < nsc; ++k) {
+    const uint32_t slot = k % kScRing;
+    const uint32_t sz = sc_wait(&S.rsize[slot], [](uint32_t v) { return v != 0; }, err, 4u) - 1;
+    if (err) break;
+    sc_copy_out(dst + o, S.ring[slot], sz, lane);
+    o += sz;
+    // (this wave's slot reads are issued before these writes, and LDS runs them in order)
+    __hip_atomic_store(&S.rsize[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&S.rseq[slot], k + kScRing, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  const uint32_t h = hv + (n ? literal_tag_bytes(n) : 0u);
+  if (!err && n && o > h + n) {  // one literal: the tag after the varint, the block from LDS
+    uint8_t* const g = dst + hv;
+    const uint32_t tb = h - hv, len = tb + n;  // literal stream bytes j: the tag (j < tb), then blk[j - tb]
+    const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
+    uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
+    const uint32_t u1 = (len + ad) >> 4;              // units [ua, u1) are whole and past the tag
+    const uint32_t ua = (tb + ad + 15) >> 4;
+    for (uint32_t u = ua + lane; u < u1; u += 64) g16[u] = sc_ld128(S.blk, 16 * u - ad - tb);
+    const uint32_t he = ua < u1 ? 16 * ua - ad : len;  // bytes [0, he) and [te, len) one by one
+    const uint32_t te = ua < u1 ? 16 * u1 - ad : len;
+    for (uint32_t j = lane; j < he + (len - te); j += 64) {
+      const uint32_t jj = j < he ? j : te + (j - he);
+      uint8_t c;
+      if (jj < tb) {
+        c = tb == 1 ? (uint8_t)((n - 1) << 2) : (jj == 0 ? (uint8_t)((58 + tb) << 2) : (uint8_t)((n - 1) >> (8 * (jj - 1))));
+      } else {
+        c = S.blk[jj - tb];
+      }
+      g[jj] = c;
+    }
+    o = h + n;
+  }
+  err |= uniform(__hip_atomic_load(&S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+  if (lane == 0) a.out_len[b] = err ? 0xfff00000u | err : o;  // (an error mark: > any block's length)
 }
 
 // Persistent: one workgroup per CU walks blocks blockIdx.x, + gridDim.x, ...; each wave loads its
@@ -636,10 +705,12 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
     }
     const uint32_t hv = a.header ? varint_len(n) : 0u;
     if (tid < hv) dst[tid] = (uint8_t)(((n >> (7 * tid)) & 0x7f) | (tid + 1 < hv ? 0x80 : 0));
-    if (wave == 0) {  // (the previous block's hand-off words were read by wave 0 before the barrier)
-      S.base[lane] = lane == 0 ? hv + 1 : 0u;
+    if (wave == 0) {  // the hand-off words (the previous block's users are past the barrier)
+      if (lane < kScRing) {
+        S.rsize[lane] = 0;
+        S.rseq[lane] = lane;
+      }
       if (lane == 0) {
-        S.base[64] = 0;
         S.ins = 0;
         S.next = 0;
         S.err = 0;
@@ -650,19 +721,20 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
     __syncthreads();
 
     const uint32_t nsc = (n + kScS - 1) / kScS;
-    for (;;) {
-      uint32_t k = 0;
-      if (lane == 0) k = __hip_atomic_fetch_add(&S.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      k = readlane(k, 0);
-      if (k >= nsc) break;
-      sc_superchunk(S, k, n, dst, wave, lane);
+    if (wave == kScWorkers) {
+      sc_writer(S, a, b, n, dst, hv, nsc, lane);
+    } else {
+      // (no lane-0-only code here or at the end of a super-chunk: the compiler merged two such
+      // regions across the loop's back edge into a divergent loop that hung the wave)
+      for (;;) {
+        // every lane adds 1 (one ds_add of 64 after the atomic optimizer); lane 0 sees a multiple of 64
+        const uint32_t k = uniform(__hip_atomic_fetch_add(&S.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 6;
+        if (k >= nsc) break;
+        sc_superchunk(S, k, n, wave, lane);
+      }
     }
     SC_FETCH(bn)  // the next block's bytes, in flight behind the other waves' last super-chunks
     __syncthreads();
-    if (wave == 0) {  // this block's result, read before wave 0 re-initialises the hand-off words
-      const uint32_t fin = S.base[nsc], er = S.err;
-      if (lane == 0) a.out_len[b] = er ? 0xffffffffu : fin - 1;
-    }
     b = bn;
   }
 #undef SC_FETCH

@@ -90,3 +90,94 @@ def test_sharded_stream_hip_compressor(oracle, gpu_available, fname, mode):
     if mode == "reference":
         assert outs[0] == oracle.compress(raw)
     assert oracle.uncompress(outs[0]) == raw
+
+
+def _config5_worker(rank, world, port, q):
+    """One rank of the config-5 stream: its contiguous fragments through
+    compress_fragments_device, the global offsets through stream_offsets_device (the gathered
+    u32 sizes), its compressed bytes placed at those offsets."""
+    import torch
+    import torch.distributed as dist
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        sm = load_package()
+        from importlib import import_module
+        D = import_module("snappy_jl_amd.dist")
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        big = bench.large_corpus()
+        nfrag = (big.size + bench.BLOCK - 1) // bench.BLOCK
+        lo, hi = D.shard_range(nfrag, rank, world)
+        sh = bench.StreamShard(big, lo, hi, dev)
+        sh.compress(sm)
+        torch.cuda.synchronize()
+        sizes = sh.comp_len.to(torch.int64).cpu()  # gloo: the size all-gather on CPU tensors
+        offs, total_c = D.stream_offsets_device(sizes, big.size, rank, world)
+        comp = sh.d_comp.cpu().numpy()
+        local = [(int(offs[i]), comp[i * bench.SLOT: i * bench.SLOT + int(sizes[i])].tobytes())
+                 for i in range(hi - lo)]
+        # the ranks' pieces to rank 0 as byte tensors (gloo all_gather needs equal shapes: pad)
+        blob = np.frombuffer(b"".join(p for _, p in local), dtype=np.uint8)
+        n = torch.tensor([blob.size], dtype=torch.int64)
+        ns = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(ns, n)
+        m = int(max(int(x) for x in ns))
+        pad = torch.zeros(m, dtype=torch.uint8)
+        pad[: blob.size] = torch.from_numpy(blob.copy())
+        parts = [torch.zeros(m, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, pad)
+        first = torch.tensor([local[0][0]], dtype=torch.int64)
+        firsts = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(firsts, first)
+        if rank == 0:
+            stream = bytearray(int(total_c.item()))
+            hdr = D.varint32(big.size)
+            stream[: len(hdr)] = hdr
+            for r in range(world):
+                o, k = int(firsts[r].item()), int(ns[r].item())
+                stream[o: o + k] = parts[r][:k].numpy().tobytes()
+            q.put((hi - lo, bytes(stream)))
+        else:
+            q.put((hi - lo, None))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config5_sharded_two_ranks(oracle, gpu_available):
+    """The 644 MiB config-5 stream's 10,304 fragments sharded over two gloo ranks on GPU 0
+    (5,152 each): the assembled stream is byte-identical to the single-GPU fragment output and
+    decodes under the oracle."""
+    import hashlib
+    import torch
+    sys.path.insert(0, ROOT)
+    import bench
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_config5_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert sorted(r[0] for r in res) == [5152, 5152]
+    sharded = [r[1] for r in res if r[1] is not None][0]
+    # the single-GPU fragment output of the same stream
+    sm = load_package()
+    dev = torch.device("cuda", 0)
+    big = bench.large_corpus()
+    sh = bench.StreamShard(big, 0, 10304, dev)
+    sh.compress(sm)
+    torch.cuda.synchronize()
+    sizes = sh.comp_len.cpu().numpy().astype(np.int64)
+    comp = sh.d_comp.cpu().numpy()
+    hdr = bytes(sm.encode32(big.size))
+    single = hdr + b"".join(comp[i * bench.SLOT: i * bench.SLOT + int(sizes[i])].tobytes() for i in range(10304))
+    assert hashlib.sha256(sharded).digest() == hashlib.sha256(single).digest()
+    assert oracle.uncompress(sharded) == big.tobytes()

@@ -41,3 +41,22 @@ def test_kernel_register_budgets(tmp_path):
         assert usage[k]["VGPRs"] < 128 and usage[k]["VGPRs Spill"] == 0, (k, usage[k])
     dec = [k for k in usage if k.endswith("k_decompressENS_14DecompressArgsE")]
     assert dec and usage[dec[0]]["Occupancy [waves/SIMD]"] >= 7, usage.get(dec[0] if dec else None)
+
+
+def test_bench_visible_gpus_from_sysfs(monkeypatch):
+    """bench.py counts GPUs without the GPU runtime (sysfs KFD topology), narrowed by the
+    *_VISIBLE_DEVICES variables, and refuses to spawn ranks once the runtime is initialised."""
+    import importlib
+    import sys
+    import types
+    sys.path.insert(0, ROOT)
+    bench = importlib.import_module("bench")
+    n = bench.visible_gpus()
+    assert n >= 0
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpus() == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    fake = types.SimpleNamespace(cuda=types.SimpleNamespace(is_initialized=lambda: True))
+    monkeypatch.setitem(sys.modules, "torch", fake)
+    args = types.SimpleNamespace(gpus=2)
+    assert bench.launch_ranks(args) == 2

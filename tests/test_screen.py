@@ -123,3 +123,30 @@ def test_screen_on_incompressible_corpus(sm, oracle, gpu_available, fname):
             s = out[out_off[b]:out_off[b] + lens[b]].tobytes()
             assert oracle.uncompress(s) == blk
             assert lens[b] <= len(oracle.compress(blk)) + len(blk) // 1000 + 8
+
+
+def test_screen_long_range_repeats(sm, oracle, gpu_available):
+    """repeats far apart (random content of period 4-48 KiB, a block made of
+    two copies of one random 32 KiB half, a record file with a 64-B header every 1 KiB) are
+    compressed, not screened as literal: each fast-mode stream is at most 1.1x the reference's
+    (oracle) size + 64 B and decodes under the oracle."""
+    rng = np.random.default_rng(2024)
+    blocks, names = [], []
+    for period in (4096, 8192, 16384, 32768, 49152):
+        seg = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+        blocks.append((seg * (65536 // period + 1))[:65536])
+        names.append("period %d" % period)
+    half = rng.integers(0, 256, 32768, dtype=np.uint8).tobytes()
+    blocks.append(half + half)
+    names.append("two halves")
+    header = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    rec = b"".join(header + rng.integers(0, 256, 960, dtype=np.uint8).tobytes() for _ in range(64))
+    blocks.append(rec)
+    names.append("64-B header every 1 KiB")
+    out, out_off, lens = _run(sm, blocks, [0] * len(blocks), [0] * len(blocks), True)
+    for b, blk in enumerate(blocks):
+        s = out[out_off[b]:out_off[b] + lens[b]].tobytes()
+        assert oracle.uncompress(s) == blk, names[b]
+        ref = len(oracle.compress(blk))
+        print("%-26s fast %6d  reference %6d" % (names[b], lens[b], ref))
+        assert lens[b] <= 1.1 * ref + 64, (names[b], lens[b], ref)
