@@ -46,7 +46,9 @@ constexpr uint32_t kScWorkers = kScW - 1;
 constexpr uint32_t kScRing = 8;           // staging slots between the workers and the writer
 constexpr uint32_t kScSlot = 1280;        // bytes per slot (a super-chunk's output is at most ~1.1 KiB)
 constexpr uint32_t kScThreads = 64 * kScW;
-constexpr uint32_t kScTabBits = 13;       // 8 K dwords = 16 K u16 slots
+constexpr uint32_t kScTabBits = 13;       // 8 K dword buckets of two u16 slots
+constexpr uint32_t kScTabWords = 1u << kScTabBits;
+constexpr uint32_t kScExt = 17;           // length byte: the 16-byte window was full (the walk extends it)
 constexpr uint32_t kScMaxL = 255;         // longest copy token (u8 lengths)
 #ifndef SC_SPIN_BITS
 #define SC_SPIN_BITS 22
@@ -56,7 +58,8 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 
 // Diagnostic builds only (-DSC_ABL=bits, tools/sc_abl.py): 1 no emission (G1, G2), 2 no resync
 // (first walks only), 4 no 16-byte choice between two full candidates, 8 no candidates (the
-// verify reads nothing), 16 no insert-token wait, 32 no base wait.  The output is not valid.
+// verify reads nothing), 16 no insert-token wait, 32 no writer copy-out, 64 no walks (every row
+// literals).  The output is not valid.
 #ifndef SC_ABL
 #define SC_ABL 0
 #endif
@@ -74,7 +77,7 @@ struct ScWaveLds {
 };
 struct ScLds {
   uint8_t blk[kBlockSize + 64];        // the block (+ pad: reads run up to 20 bytes past a position)
-  uint32_t T[(1u << kScTabBits) + 4];  // hash table; T[1 << kScTabBits] is the dummy for invalid lanes
+  uint32_t T[kScTabWords + 4];         // hash table (two u16 slots a dword); T[kScTabWords] is the dummy for invalid lanes
   ScWaveLds w[kScWorkers];
   uint8_t ring[kScRing][kScSlot];      // staged outputs: super-chunk k in slot k % kScRing
   uint64_t M[kScWorkers][kScG];        // per worker: match bitmask (bit = position of the super-chunk)
@@ -190,6 +193,25 @@ __device__ inline uint32_t sc_extend(const uint8_t* blk, uint32_t q, uint32_t of
   }
 }
 
+// lowest set bit of x, ~0 for 0 (v_ffbl_b32)
+__device__ inline uint32_t sc_ffbl(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));  // (the compiler does not know ffbl(0) = ~0)
+  return r;
+}
+
+// equal leading bytes (0..16) of the 16 bytes X0..X3 and the 16 bytes at w + s (s < 4; w dword-aligned LDS)
+__device__ __attribute__((always_inline)) inline uint32_t sc_eq16(uint32_t X0, uint32_t X1, uint32_t X2, uint32_t X3,
+                                                                  const uint32_t* w, uint32_t s) {
+  const uint32_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3], a4 = w[4];
+  // first differing bit (ffbl(0) = ~0 survives the | and loses the min)
+  const uint32_t b0 = sc_ffbl(X0 ^ __builtin_amdgcn_alignbyte(a1, a0, s));
+  const uint32_t b1 = sc_ffbl(X1 ^ __builtin_amdgcn_alignbyte(a2, a1, s)) | 32u;
+  const uint32_t b2 = sc_ffbl(X2 ^ __builtin_amdgcn_alignbyte(a3, a2, s)) | 64u;
+  const uint32_t b3 = sc_ffbl(X3 ^ __builtin_amdgcn_alignbyte(a4, a3, s)) | 96u;
+  return min(min(b0, b1), min(min(b2, b3), 128u)) >> 3;
+}
+
 // c ? a : b on values (a conditional on lvalues can become a select of their addresses)
 __device__ inline uint32_t sc_sel(uint32_t c, uint32_t a, uint32_t b) { return c ? a : b; }
 
@@ -222,7 +244,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   const uint32_t sc0 = k * kScS, sce = min(sc0 + kScS, n);
   const uint32_t Tbase = lds_addr(S.T);
   STAMP_DECL
-  // ---- A. hashes of the 16 groups: LDS byte address of the bucket, slot value ----
+  // ---- A. hashes of the 16 groups: LDS byte address of the bucket dword, the slot value ----
   uint32_t ha[kScG], hvv[kScG];
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
@@ -230,7 +252,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, (q & ~3u) + 4), sc_ld32(S.blk, q & ~3u), q & 3u);
     const uint32_t h = (w * kHashMul) >> (32 - kScTabBits);
     const bool valid = q + 4 <= n;
-    ha[g] = Tbase + 4 * (valid ? h : (1u << kScTabBits));
+    ha[g] = Tbase + 4 * (valid ? h : kScTabWords);
     hvv[g] = (q + 1) << (16 * (g & 1));
   }
   const uint32_t mk0 = 0xffffu, mk1 = 0xffff0000u;
@@ -278,7 +300,9 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   __builtin_amdgcn_s_setprio(0);
   STAMP(2)
 
-  // ---- C. verify both candidates of every position ----
+  // ---- C. verify both candidates of every position over 16 bytes, keep the longer (branch-free:
+  // the loads for a missing candidate read the position's own bytes, and its length is masked) ----
+  uint64_t mbs[kScG];
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
     const uint32_t q = sc0 + 64 * g + lane;
@@ -292,127 +316,110 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t* wq = reinterpret_cast<const uint32_t*>(S.blk + (q & ~3u));
     const uint32_t* w1 = reinterpret_cast<const uint32_t*>(S.blk + (p1 & ~3u));
     const uint32_t* w2 = reinterpret_cast<const uint32_t*>(S.blk + (p2 & ~3u));
-    const uint32_t x0 = wq[0], x1 = wq[1], x2 = wq[2];
-    const uint32_t a0 = w1[0], a1 = w1[1], a2 = w1[2];
-    const uint32_t b0 = w2[0], b1 = w2[1], b2 = w2[2];
     const uint32_t sq = q & 3u, s1 = p1 & 3u, s2 = p2 & 3u;
+    const uint32_t x0 = wq[0], x1 = wq[1], x2 = wq[2], x3 = wq[3], x4 = wq[4];
     const uint32_t X0 = __builtin_amdgcn_alignbyte(x1, x0, sq), X1 = __builtin_amdgcn_alignbyte(x2, x1, sq);
-    uint32_t l1 = ok1 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(a1, a0, s1), __builtin_amdgcn_alignbyte(a2, a1, s1)) : 0u;
-    uint32_t l2 = ok2 ? sc_diff8(X0, X1, __builtin_amdgcn_alignbyte(b1, b0, s2), __builtin_amdgcn_alignbyte(b2, b1, s2)) : 0u;
-    uint32_t win = 8;
-    // both fill the window: compare the next 8 bytes to choose (the longer match wins)
-    const bool both = !(SC_ABL & 4) && l1 == 8 && l2 == 8 && avail > 8;
-    if (ballot(both)) {
-      if (both) {
-        const uint32_t x3 = wq[3], x4 = wq[4], a3 = w1[3], a4 = w1[4], b3 = w2[3], b4 = w2[4];
-        const uint32_t X2 = __builtin_amdgcn_alignbyte(x3, x2, sq), X3 = __builtin_amdgcn_alignbyte(x4, x3, sq);
-        l1 += sc_diff8(X2, X3, __builtin_amdgcn_alignbyte(a3, a2, s1), __builtin_amdgcn_alignbyte(a4, a3, s1));
-        l2 += sc_diff8(X2, X3, __builtin_amdgcn_alignbyte(b3, b2, s2), __builtin_amdgcn_alignbyte(b4, b3, s2));
-        win = 16;
-      }
-    }
-    const bool take2 = l2 > l1;  // ties: the latest (shorter offset)
-    const uint32_t l = take2 ? l2 : l1, c = take2 ? p2 : p1;
+    const uint32_t X2 = __builtin_amdgcn_alignbyte(x3, x2, sq), X3 = __builtin_amdgcn_alignbyte(x4, x3, sq);
+    uint32_t lw1 = sc_eq16(X0, X1, X2, X3, w1, s1), lw2 = sc_eq16(X0, X1, X2, X3, w2, s2);
+    asm("" : "+v"(lw1), "+v"(lw2));  // (keeps the loads unconditional: no branch around them)
+    const uint32_t l1 = ok1 ? lw1 : 0u, l2 = ok2 ? lw2 : 0u;
+    const bool take2 = l2 > l1;  // ties: the later candidate (shorter offset)
+    const uint32_t l = take2 ? l2 : l1, p = take2 ? p2 : p1;
     const uint32_t L = min(l, avail);
     const bool match = L >= 4;
-    const bool ext = l == win && avail > win;  // the window was full: the walk extends it
-    const uint32_t enc = !match ? 0u : (ext ? win >> 3 : L);
+    const uint32_t enc = !match ? 0u : ((l == 16 && avail > 16) ? kScExt : L);
     const uint32_t pos = 64 * g + lane;  // row pos / 16, entry pos % 16
     Wl.L[pos] = (uint8_t)enc;
     uint16_t* const Orow = (lane & 8) ? Wl.Ohi : Wl.Olo;
-    Orow[(pos >> 4) * 8 + (lane & 7)] = (uint16_t)(q - c);
-    const uint64_t mb = ballot(match);
-    if (lane == 0) S.M[wave][g] = mb;
+    Orow[(pos >> 4) * 8 + (lane & 7)] = (uint16_t)(q - p);
+    mbs[g] = ballot(match);
+  }
+  if (lane == 0) {  // (one branch after the groups: a branch per group would stop their overlap)
+#pragma unroll
+    for (int g = 0; g < (int)kScG; ++g) S.M[wave][g] = mbs[g];
   }
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   STAMP(3)
 
-  // ---- D. lane-serial walks over the row in registers, resynchronised ----
+  // ---- D. lane-serial walks over the row, resynchronised ----
+  // A lane's row: the match bitmask, the length bytes (4..16 exact, kScExt: extend from 16) and
+  // per position the next token of the greedy walk after a token there (packed nibbles: 0 = the
+  // token leaves the row or only literals follow).  A walk is then <= 4 nibble steps.
   const uint32_t c0 = sc0 + kScC * lane;
   const uint32_t ce = c0 < sce ? min(c0 + kScC, sce) : c0;
   const uint32_t mask16 = reinterpret_cast<const uint16_t*>(S.M[wave])[lane];
-  // the row in scalars (a select between aggregates would make the compiler address them in memory)
   uint32_t l0, l1, l2, l3;
   {
     const uint4 v = reinterpret_cast<const uint4*>(Wl.L)[lane];
     l0 = v.x, l1 = v.y, l2 = v.z, l3 = v.w;
   }
-  const uint4 Olr = reinterpret_cast<const uint4*>(Wl.Olo)[lane], Ohr = reinterpret_cast<const uint4*>(Wl.Ohi)[lane];
-  const uint32_t o0 = Olr.x, o1 = Olr.y, o2 = Olr.z, o3 = Olr.w, o4 = Ohr.x, o5 = Ohr.y, o6 = Ohr.z, o7 = Ohr.w;
+  uint32_t jlo = 0, jhi = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t li = ((i < 4 ? l0 : i < 8 ? l1 : i < 12 ? l2 : l3) >> (8 * (i & 3))) & 0xffu;
+    const uint32_t t = i + min(li, 16u);  // <= 31: mask16 >> t is 0 past the row
+    const uint32_t m = mask16 >> t;
+    const uint32_t jn = m ? t + (uint32_t)__builtin_ctz(m) : 0u;
+    if (i < 8)
+      jlo |= jn << (4 * i);
+    else
+      jhi |= jn << (4 * (i - 8));
+  }
   auto getL = [&](uint32_t i) -> uint32_t {
     const uint32_t d = sc_sel(i & 8, sc_sel(i & 4, l3, l2), sc_sel(i & 4, l1, l0));
     return (d >> (8 * (i & 3))) & 0xffu;
   };
-  auto setL = [&](uint32_t i, uint32_t v) {  // (after an extension: later walks of this super-chunk reuse it)
-    const uint32_t sb = 8 * (i & 3), m = ~(0xffu << sb), x = v << sb, j = i >> 2;
-    l0 = j == 0 ? (l0 & m) | x : l0;
-    l1 = j == 1 ? (l1 & m) | x : l1;
-    l2 = j == 2 ? (l2 & m) | x : l2;
-    l3 = j == 3 ? (l3 & m) | x : l3;
-  };
-  auto getO = [&](uint32_t i) -> uint32_t {
-    const uint32_t hi = i & 8;
-    const uint32_t hx = sc_sel(hi, o4, o0), hy = sc_sel(hi, o5, o1), hz = sc_sel(hi, o6, o2), hw = sc_sel(hi, o7, o3);
-    const uint32_t d = sc_sel(i & 4, sc_sel(i & 2, hw, hz), sc_sel(i & 2, hy, hx));
-    return (d >> (16 * (i & 1))) & 0xffffu;
-  };
-  // Walk from s (c0 <= s < ce) until the walk lands on a position of `stop` (the lane's old path)
-  // or leaves the row: new tokens in nt, the path positions in newP, the end (or merge) position.
-  auto walk = [&](uint32_t s, uint32_t stop, ScToks& nt, uint32_t& newP, uint32_t& pend, bool& merged) __attribute__((always_inline)) {
-    nt.n = 0;
-    nt.t[0] = nt.t[1] = nt.t[2] = nt.t[3] = 0;
-    newP = 0;
-    merged = false;
-    uint32_t p = s;
-    bool act = true;
+  // the last token's extended length (one per lane: resync walks often end on the same token)
+  uint32_t xpos = 16, xlen = 0;
+  // Walk from row position sr (16: none) until the walk leaves the row or lands on a token of
+  // `stop`: the token bits, the merge position (16: none), the lane's end position.
+  auto walk = [&](uint32_t sr, uint32_t stop, uint32_t& path, uint32_t& mpos, uint32_t& pend) __attribute__((always_inline)) {
+    const uint32_t m0 = sr < 16 ? mask16 >> sr : 0u;
+    uint32_t i = m0 ? sr + (uint32_t)__builtin_ctz(m0) : 16u;
+    path = 0;
+    mpos = 16;
+    uint32_t last = 16;
+    bool act = i < 16;
     while (ballot(act)) {
       if (act) {
-        const uint32_t rel = p - c0;
-        const uint32_t m = mask16 >> rel;
-        const uint32_t t = m ? (uint32_t)__builtin_ctz(m) : ce - p;  // literals before the next match
-        const uint32_t sb = (stop >> rel) & ((2u << t) - 1u);         // old-path positions in [p, p + t]
-        if (sb) {  // lands on the old path: from here the walks are the same
-          const uint32_t d = (uint32_t)__builtin_ctz(sb);
-          newP |= sc_bits(rel, rel + d);
-          p += d;
-          merged = true;
-          act = false;
-        } else if (!m) {  // literals to the end of the row
-          newP |= sc_bits(rel, ce - c0);
-          p = ce;
+        if ((stop >> i) & 1u) {
+          mpos = i;
           act = false;
         } else {
-          const uint32_t i = rel + t;
-          newP |= sc_bits(rel, i + 1);
-          uint32_t L = getL(i);
-          const uint32_t off = getO(i);
-          if (L < 4) {  // the verified window was full: extend
-            L = sc_extend(S.blk, c0 + i, off, L == 1 ? 8u : 16u, min(kScMaxL, sce - (c0 + i)));
-            setL(i, L);
-          }
-          const uint32_t tv = off | (L << 16) | (i << 24);
-          nt.t[0] = nt.n == 0 ? tv : nt.t[0];
-          nt.t[1] = nt.n == 1 ? tv : nt.t[1];
-          nt.t[2] = nt.n == 2 ? tv : nt.t[2];
-          nt.t[3] = nt.n == 3 ? tv : nt.t[3];
-          ++nt.n;
-          p = c0 + i + L;
-          act = p < ce;
+          path |= 1u << i;
+          last = i;
+          const uint32_t j = (uint32_t)((((uint64_t)jhi << 32) | jlo) >> (4 * i)) & 0xfu;
+          act = j != 0;
+          i = j;
         }
       }
     }
-    pend = p;
+    // the end: the last token's end when it leaves the row, else the row end (literals follow)
+    pend = ce;
+    if (last < 16) {
+      uint32_t L = getL(last);
+      const bool ext = L == kScExt;
+      if (last + min(L, 16u) >= 16) {
+        if (ballot(ext)) {
+          if (ext) {
+            if (xpos != last) {
+              const uint16_t* Orow = (last & 8) ? Wl.Ohi : Wl.Olo;
+              xlen = sc_extend(S.blk, c0 + last, Orow[lane * 8 + (last & 7)], 16u, min(kScMaxL, sce - (c0 + last)));
+              xpos = last;
+            }
+            L = xlen;
+          }
+        }
+        pend = c0 + last + L;
+      }
+    }
   };
   const bool row = c0 < sce;  // the lane has positions
   uint32_t s = c0, e, P;
-  ScToks tk;
   {
-    bool mg;
-    walk(row ? c0 : ce, 0u, tk, P, e, mg);
-    if (!row) {
-      tk.n = 0;
-      e = c0;
-    }
+    uint32_t mp;
+    walk(row ? 0u : 16u, 0u, P, mp, e);
+    if (!row) e = c0;
   }
   for (; !(SC_ABL & 2);) {
     const uint32_t pe = __builtin_amdgcn_update_dpp(0u, e, 0x138, 0xf, 0xf, false);  // wave_shr:1
@@ -420,36 +427,36 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const bool chg = sn != s;
     if (!ballot(chg)) break;
     STAMP_COUNT(10, 1)
-    const bool inrow = chg && sn >= c0 && sn < ce;
-    ScToks nt;
-    uint32_t nP, m;
-    bool mg;
-    walk(inrow ? sn : ce, P & ~sc_bits(0, inrow ? sn - c0 : 0), nt, nP, m, mg);  // (rows not walking: stop at once)
+    const bool inrow = chg && sn < ce;  // (an entry is never before the row)
+    uint32_t nP, mp, ne;
+    walk(inrow ? sn - c0 : 16u, P, nP, mp, ne);  // (rows not walking: stop at once)
     if (chg) {
       s = sn;
       if (!inrow) {  // past the row (a copy jumped over it) or a lane without positions
-        tk.n = 0;
         P = 0;
         e = sn;
-      } else if (!mg) {
-        tk = nt;
+      } else if (mp == 16) {
         P = nP;
-        e = m;
+        e = ne;
       } else {  // the new tokens, then the old ones from the merge position on (e unchanged)
-        const uint32_t mi = m - c0;
-        uint32_t d = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) d += ((uint32_t)j < tk.n && (tk.t[j] >> 24) < mi) ? 1u : 0u;
-        ScToks o = tk;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t x = j - nt.n + d;  // old index for slot j >= nt.n
-          const uint32_t ov = x == 0 ? o.t[0] : (x == 1 ? o.t[1] : (x == 2 ? o.t[2] : o.t[3]));
-          tk.t[j] = (uint32_t)j < nt.n ? nt.t[j] : ov;
-        }
-        tk.n = nt.n + o.n - d;
-        P = nP | (P & ~sc_bits(0, mi));
+        P = nP | (P & ~sc_bits(0, mp));
       }
+    }
+  }
+  // the lane's tokens from its token bits: offset | length << 16 | position-in-row << 24
+  ScToks tk;
+  {
+    uint32_t pm = P;
+    tk.n = (uint32_t)__builtin_popcount(P);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t i = pm ? (uint32_t)__builtin_ctz(pm) : 0u;
+      pm &= pm - 1;
+      uint32_t L = getL(i);
+      L = L == kScExt ? xlen : L;  // (only the last token can be an extended one, and it was)
+      const uint16_t* Orow = (i & 8) ? Wl.Ohi : Wl.Olo;
+      const uint32_t off = Orow[lane * 8 + (i & 7)];
+      tk.t[j] = off | (L << 16) | (i << 24);
     }
   }
   STAMP(4)
@@ -611,7 +618,7 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, const 
     const uint32_t slot = k % kScRing;
     const uint32_t sz = sc_wait(&S.rsize[slot], [](uint32_t v) { return v != 0; }, err, 4u) - 1;
     if (err) break;
-    sc_copy_out(dst + o, S.ring[slot], sz, lane);
+    if (!(SC_ABL & 32)) sc_copy_out(dst + o, S.ring[slot], sz, lane);
     o += sz;
     // (this wave's slot reads are issued before these writes, and LDS runs them in order)
     __hip_atomic_store(&S.rsize[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -701,7 +708,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
     if (tid < 64) S.blk[n + tid] = 0;  // bytes past the block read as zeros (never part of a match)
     {
       uint4* t16 = reinterpret_cast<uint4*>(S.T);
-      for (uint32_t k = tid; k < (4u << kScTabBits) / 16; k += kScThreads) t16[k] = make_uint4(0, 0, 0, 0);
+      for (uint32_t k = tid; k < 4 * kScTabWords / 16; k += kScThreads) t16[k] = make_uint4(0, 0, 0, 0);
     }
     const uint32_t hv = a.header ? varint_len(n) : 0u;
     if (tid < hv) dst[tid] = (uint8_t)(((n >> (7 * tid)) & 0x7f) | (tid + 1 < hv ? 0x80 : 0));

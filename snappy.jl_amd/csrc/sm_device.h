@@ -28,6 +28,12 @@ namespace sm {
 #define STAMP_FLUSH(arr) \
   if (lane == 0)         \
     for (int i_ = 0; i_ < kStampSlots; ++i_) atomicAdd(&arr[i_], (unsigned long long)st_acc[i_]);
+#elif defined(SM_MARKS)  // static listing only (-DSM_MARKS -S): section marks in the assembly
+#define STAMP_MACROS(NS)
+#define STAMP_DECL
+#define STAMP(i) asm volatile("; SCMARK " #i);
+#define STAMP_COUNT(i, v)
+#define STAMP_FLUSH(arr)
 #else
 #define STAMP_MACROS(NS)
 #define STAMP_DECL

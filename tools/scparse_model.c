@@ -18,7 +18,7 @@ static uint32_t copy_bytes(uint32_t off, uint32_t len) {
   if (len > 64) { b += 3; len -= 60; }
   return b + ((len < 12 && off < 2048) ? 2 : 3);
 }
-static int REFH = 0, DEPTH = 1, PREF8 = 0, TIE2 = 0, PAR = 0;
+static int REFH = 0, DEPTH = 1, PREF8 = 0, TIE2 = 0, PAR = 0, ROW = 0;
 static uint32_t hsh(uint32_t w, int bits) {
   if (REFH) return (w * 0x1e35a7bdu) >> (32 - bits);
   return ((((w ^ (w >> 12)) & 0xffffff) * 0x1e35a7u) >> 10) & ((1u << bits) - 1); }
@@ -27,10 +27,16 @@ static uint32_t vlen(uint32_t v) { return v < 128 ? 1 : v < 16384 ? 2 : v < (1u 
 static uint64_t block_size(const uint8_t* d, uint32_t n, uint32_t S, int tb, uint32_t lcap, int header) {
   static uint32_t T[1 << 16], prev[65536], prev2[65536], T2[1<<16];
   memset(T, 0, sizeof(uint32_t) << tb); memset(T2, 0, sizeof(uint32_t) << tb);
-  for (uint32_t q = 0; q + 4 <= n; ++q) {
+  for (uint32_t qi = 0; qi < n; ++qi) {
+    uint32_t q = qi;
+    if (ROW) {  // super-chunk by super-chunk; inside one: position-in-row j, then row (lane) order
+      const uint32_t sc = qi / S * S, r = qi - sc, j = r / (S / 16), lane = r % (S / 16);
+      q = sc + 16 * lane + j;
+    }
+    if (q + 4 > n) { prev[q] = prev2[q] = 0; continue; }
     uint32_t h = hsh(ld32(d + q), tb);
     if (PAR) {  // two tables by parity class: exchange own class, read the other
-      uint32_t cls = PAR == 1 ? (q & 1) : ((q >> 6) & 1);
+      uint32_t cls = PAR == 1 ? (q & 1) : ((q >> 6) & 1);  // (ROW: q & 1 is the instruction parity)
       uint32_t* Ta = cls ? T2 : T;
       uint32_t* Tb = cls ? T : T2;
       uint32_t a = Ta[h], bb = Tb[h];
@@ -53,6 +59,7 @@ static uint64_t block_size(const uint8_t* d, uint32_t n, uint32_t S, int tb, uin
       for (int k = 0; k < DEPTH; ++k) {
         uint32_t pv = k ? prev2[p] : prev[p];
         if (p + 4 <= s1 && pv) {
+          if (pv - 1 >= p) continue;  // (ROW order: a later position can be in the table)
           uint32_t c = pv - 1, lim = s1 - p < lcap ? s1 - p : lcap, l = 0;
           uint32_t lim8 = PREF8 && lim > (uint32_t)PREF8 ? (uint32_t)PREF8 : lim;
           while (l < lim8 && d[c + l] == d[p + l]) ++l;
@@ -82,6 +89,7 @@ int main(int argc, char** argv) {
   int tb = atoi(argv[2]);
   if (getenv("REFH")) REFH = 1;
   if (getenv("TIE2")) TIE2 = 1;
+  if (getenv("ROW")) ROW = 1;
   if (getenv("PAR")) PAR = atoi(getenv("PAR"));
   if (getenv("DEPTH")) DEPTH = atoi(getenv("DEPTH"));
   if (getenv("PREF8")) PREF8 = atoi(getenv("PREF8"));
