@@ -71,9 +71,9 @@ STAMP_MACROS(12)
 
 // per-wave LDS: rows of 16 positions (row r = lane r's positions)
 struct ScWaveLds {
-  uint8_t L[kScS];         // match length byte per position (0: none; 1/2: extend from 8/16)
-  uint16_t Olo[kScS / 2];  // offsets of positions 0..7 of each row
-  uint16_t Ohi[kScS / 2];  // offsets of positions 8..15 of each row
+  uint8_t L[kScS];   // match length per walked position (4..16; kScExt: extend from 16), rows of 16
+                     // bytes, the row's dwords swizzled by (row >> 3) & 3 (conflict-free byte stores)
+  uint16_t O[kScS];  // candidate offset per position, rows of 16, dword pairs swizzled by (row >> 2) & 7
 };
 struct ScLds {
   uint8_t blk[kBlockSize + 64];        // the block (+ pad: reads run up to 20 bytes past a position)
@@ -300,8 +300,12 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   __builtin_amdgcn_s_setprio(0);
   STAMP(2)
 
-  // ---- C. verify both candidates of every position over 16 bytes, keep the longer (branch-free:
-  // the loads for a missing candidate read the position's own bytes, and its length is masked) ----
+  // ---- C. one candidate per position: the latest earlier position of the same hash (own slot or
+  // the other's, the more recent first) whose first 4 bytes equal the position's.  Only its offset
+  // is stored (row-major, swizzled); match lengths are computed by the walks (D), and only at the
+  // positions a walk visits.  (Choosing the longer of the two by an 8-byte compare instead gives
+  // ratio 0.5625 against 0.5738 on the bench text, but 3.21 against 2.96 ms, and a round trip
+  // 3.6% slower: DESIGN.md section 3.2d.) ----
   uint64_t mbs[kScG];
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
@@ -309,30 +313,16 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t sh = 16 * (g & 1);
     const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
     const uint32_t c1 = (SC_ABL & 8) ? 0u : max(ca, cb), c2 = (SC_ABL & 8) ? 0u : min(ca, cb);
-    const uint32_t avail = q < sce ? sce - q : 0u;  // bytes a match may cover (super-chunk end)
-    // (c - 1 < q also rejects c == 0; only invalid lanes -- avail < 4 -- can see other values)
-    const bool ok1 = avail >= 4 && c1 - 1 < q, ok2 = avail >= 4 && c2 - 1 < q;
+    const bool room = q + 4 <= sce;  // a match may cover 4 bytes before the super-chunk end
+    // (c - 1 < q also rejects c == 0; the loads of a rejected candidate read the position itself)
+    const bool ok1 = room && c1 - 1 < q, ok2 = room && c2 - 1 < q;
     const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
-    const uint32_t* wq = reinterpret_cast<const uint32_t*>(S.blk + (q & ~3u));
-    const uint32_t* w1 = reinterpret_cast<const uint32_t*>(S.blk + (p1 & ~3u));
-    const uint32_t* w2 = reinterpret_cast<const uint32_t*>(S.blk + (p2 & ~3u));
-    const uint32_t sq = q & 3u, s1 = p1 & 3u, s2 = p2 & 3u;
-    const uint32_t x0 = wq[0], x1 = wq[1], x2 = wq[2], x3 = wq[3], x4 = wq[4];
-    const uint32_t X0 = __builtin_amdgcn_alignbyte(x1, x0, sq), X1 = __builtin_amdgcn_alignbyte(x2, x1, sq);
-    const uint32_t X2 = __builtin_amdgcn_alignbyte(x3, x2, sq), X3 = __builtin_amdgcn_alignbyte(x4, x3, sq);
-    uint32_t lw1 = sc_eq16(X0, X1, X2, X3, w1, s1), lw2 = sc_eq16(X0, X1, X2, X3, w2, s2);
-    asm("" : "+v"(lw1), "+v"(lw2));  // (keeps the loads unconditional: no branch around them)
-    const uint32_t l1 = ok1 ? lw1 : 0u, l2 = ok2 ? lw2 : 0u;
-    const bool take2 = l2 > l1;  // ties: the later candidate (shorter offset)
-    const uint32_t l = take2 ? l2 : l1, p = take2 ? p2 : p1;
-    const uint32_t L = min(l, avail);
-    const bool match = L >= 4;
-    const uint32_t enc = !match ? 0u : ((l == 16 && avail > 16) ? kScExt : L);
-    const uint32_t pos = 64 * g + lane;  // row pos / 16, entry pos % 16
-    Wl.L[pos] = (uint8_t)enc;
-    uint16_t* const Orow = (lane & 8) ? Wl.Ohi : Wl.Olo;
-    Orow[(pos >> 4) * 8 + (lane & 7)] = (uint16_t)(q - p);
-    mbs[g] = ballot(match);
+    uint32_t v1 = lds_ld32(S.blk, p1), v2 = lds_ld32(S.blk, p2), w = lds_ld32(S.blk, q);
+    asm("" : "+v"(v1), "+v"(v2), "+v"(w));  // (keeps the loads unconditional)
+    const bool m1 = ok1 && v1 == w, m2 = ok2 && v2 == w;
+    const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
+    Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (m1 ? p1 : p2));
+    mbs[g] = ballot(m1 || m2);
   }
   if (lane == 0) {  // (one branch after the groups: a branch per group would stop their overlap)
 #pragma unroll
@@ -342,33 +332,15 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   STAMP(3)
 
   // ---- D. lane-serial walks over the row, resynchronised ----
-  // A lane's row: the match bitmask, the length bytes (4..16 exact, kScExt: extend from 16) and
-  // per position the next token of the greedy walk after a token there (packed nibbles: 0 = the
-  // token leaves the row or only literals follow).  A walk is then <= 4 nibble steps.
+  // A lane walks its row greedily: at a match position it computes the match length (16-byte
+  // compare; kScExt: the 16 bytes were equal, the walk's last token is extended), records it, and
+  // jumps to the first match position at or after the copy's end (the row's match bitmask).
   const uint32_t c0 = sc0 + kScC * lane;
   const uint32_t ce = c0 < sce ? min(c0 + kScC, sce) : c0;
   const uint32_t mask16 = reinterpret_cast<const uint16_t*>(S.M[wave])[lane];
-  uint32_t l0, l1, l2, l3;
-  {
-    const uint4 v = reinterpret_cast<const uint4*>(Wl.L)[lane];
-    l0 = v.x, l1 = v.y, l2 = v.z, l3 = v.w;
-  }
-  uint32_t jlo = 0, jhi = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const uint32_t li = ((i < 4 ? l0 : i < 8 ? l1 : i < 12 ? l2 : l3) >> (8 * (i & 3))) & 0xffu;
-    const uint32_t t = i + min(li, 16u);  // <= 31: mask16 >> t is 0 past the row
-    const uint32_t m = mask16 >> t;
-    const uint32_t jn = m ? t + (uint32_t)__builtin_ctz(m) : 0u;
-    if (i < 8)
-      jlo |= jn << (4 * i);
-    else
-      jhi |= jn << (4 * (i - 8));
-  }
-  auto getL = [&](uint32_t i) -> uint32_t {
-    const uint32_t d = sc_sel(i & 8, sc_sel(i & 4, l3, l2), sc_sel(i & 4, l1, l0));
-    return (d >> (8 * (i & 3))) & 0xffu;
-  };
+  const uint32_t osw = (lane >> 2) & 7, lsw = (lane >> 3) & 3;  // the row's swizzles
+  auto offAt = [&](uint32_t i) -> uint32_t { return Wl.O[16 * lane + 2 * ((i >> 1) ^ osw) + (i & 1)]; };
+  uint8_t* const Lrow = Wl.L + 16 * lane;
   // the last token's extended length (one per lane: resync walks often end on the same token)
   uint32_t xpos = 16, xlen = 0;
   // Walk from row position sr (16: none) until the walk leaves the row or lands on a token of
@@ -378,7 +350,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     uint32_t i = m0 ? sr + (uint32_t)__builtin_ctz(m0) : 16u;
     path = 0;
     mpos = 16;
-    uint32_t last = 16;
+    uint32_t last = 16, lastL = 0;
     bool act = i < 16;
     while (ballot(act)) {
       if (act) {
@@ -388,23 +360,31 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
         } else {
           path |= 1u << i;
           last = i;
-          const uint32_t j = (uint32_t)((((uint64_t)jhi << 32) | jlo) >> (4 * i)) & 0xfu;
-          act = j != 0;
-          i = j;
+          const uint32_t q = c0 + i, off = offAt(i);
+          const uint4 X = sc_ld128(S.blk, q);
+          const uint32_t p = q - off;
+          const uint32_t l = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p & ~3u)), p & 3u);
+          const uint32_t avail = sce - q;
+          const uint32_t enc = (l == 16 && avail > 16) ? kScExt : min(l, avail);
+          Lrow[4 * ((i >> 2) ^ lsw) + (i & 3)] = (uint8_t)enc;
+          lastL = enc;
+          const uint32_t t = i + min(enc, 16u);  // <= 31: mask16 >> t is 0 past the row
+          const uint32_t m = mask16 >> t;
+          i = m ? t + (uint32_t)__builtin_ctz(m) : 16u;
+          act = i < 16;
         }
       }
     }
     // the end: the last token's end when it leaves the row, else the row end (literals follow)
     pend = ce;
     if (last < 16) {
-      uint32_t L = getL(last);
+      uint32_t L = lastL;
       const bool ext = L == kScExt;
       if (last + min(L, 16u) >= 16) {
         if (ballot(ext)) {
           if (ext) {
             if (xpos != last) {
-              const uint16_t* Orow = (last & 8) ? Wl.Ohi : Wl.Olo;
-              xlen = sc_extend(S.blk, c0 + last, Orow[lane * 8 + (last & 7)], 16u, min(kScMaxL, sce - (c0 + last)));
+              xlen = sc_extend(S.blk, c0 + last, offAt(last), 16u, min(kScMaxL, sce - (c0 + last)));
               xpos = last;
             }
             L = xlen;
@@ -443,6 +423,17 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       }
     }
   }
+  // the lengths the walks recorded (every token of P has one)
+  uint32_t l0, l1, l2, l3;
+  {
+    const uint4 v = reinterpret_cast<const uint4*>(Wl.L)[lane];
+    l0 = v.x, l1 = v.y, l2 = v.z, l3 = v.w;
+  }
+  auto getL = [&](uint32_t i) -> uint32_t {
+    const uint32_t k = (i >> 2) ^ lsw;
+    const uint32_t d = sc_sel(k & 2, sc_sel(k & 1, l3, l2), sc_sel(k & 1, l1, l0));
+    return (d >> (8 * (i & 3))) & 0xffu;
+  };
   // the lane's tokens from its token bits: offset | length << 16 | position-in-row << 24
   ScToks tk;
   {
@@ -454,8 +445,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       pm &= pm - 1;
       uint32_t L = getL(i);
       L = L == kScExt ? xlen : L;  // (only the last token can be an extended one, and it was)
-      const uint16_t* Orow = (i & 8) ? Wl.Ohi : Wl.Olo;
-      const uint32_t off = Orow[lane * 8 + (i & 7)];
+      const uint32_t off = offAt(i);
       tk.t[j] = off | (L << 16) | (i << 24);
     }
   }
