@@ -161,6 +161,34 @@ __device__ inline void sc_lds_put3(uint8_t* p, uint32_t v, uint32_t cs) {
   if (cs > 2) p[2] = (uint8_t)(v >> 16);
 }
 
+// v with the bytes from len (0..16) on cleared
+__device__ inline uint4 sc_trim(uint4 v, uint32_t len) {
+  const uint64_t mlo = len >= 8 ? ~0ull : (1ull << (8 * (len & 7))) - 1;
+  const uint64_t mhi = len >= 16 ? ~0ull : (len <= 8 ? 0ull : (1ull << (8 * (len & 7))) - 1);
+  return make_uint4(v.x & (uint32_t)mlo, v.y & (uint32_t)(mlo >> 32), v.z & (uint32_t)mhi, v.w & (uint32_t)(mhi >> 32));
+}
+
+// ors the 16 bytes v (zero past the piece) into the zeroed LDS byte array at byte address a (any
+// alignment): five ds_or_b32, unconditionally (an or of zeros leaves a neighbour's bytes alone)
+__device__ inline void sc_lds_or(uint32_t a, uint4 v) {
+  const uint32_t sh = a & 3u, wa = a & ~3u, r = 4 - sh;  // alignbyte(hi, lo, r) = (hi:lo) >> 8r
+  const uint32_t u0 = v.x << (8 * sh);
+  const uint32_t u1 = sh ? __builtin_amdgcn_alignbyte(v.y, v.x, r) : v.y;
+  const uint32_t u2 = sh ? __builtin_amdgcn_alignbyte(v.z, v.y, r) : v.z;
+  const uint32_t u3 = sh ? __builtin_amdgcn_alignbyte(v.w, v.z, r) : v.w;
+  const uint32_t u4 = sh ? v.w >> (8 * r) : 0u;
+  asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4\nds_or_b32 %0, %3 offset:8\nds_or_b32 %0, %4 offset:12\n"
+               "ds_or_b32 %0, %5 offset:16"
+               : : "v"(wa), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4) : "memory");
+}
+
+// ors the (up to 3) bytes of cv into the zeroed LDS byte array at byte address a
+__device__ inline void sc_lds_or3(uint32_t a, uint32_t cv) {
+  const uint32_t sh = a & 3u, wa = a & ~3u;
+  const uint32_t lo = cv << (8 * sh), hi = sh ? cv >> (8 * (4 - sh)) : 0u;
+  asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
+}
+
 // v shifted up by t (0..3) bytes with the t-byte value tag below it
 __device__ inline uint4 sc_prepend(uint4 v, uint32_t tag, uint32_t t) {
   if (t == 0) return v;
@@ -480,14 +508,9 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   const bool cont = ptrail > 0 && lead > 0;  // this lane's first run continues the previous lane's last one
   const bool mid = cont && tk.n == 0;         // ... and is all the lane has: the run goes on
   const uint32_t Cs = scan_dpp(cont ? lead : 0u);
-  uint32_t f = mid ? 64u : lane;  // first lane >= this one where a run stops passing through
-#pragma unroll
-  for (uint32_t dd = 1; dd < 64; dd <<= 1) {
-    const uint32_t o2 = __shfl_down(f, dd, 64);
-    f = lane + dd < 64 ? min(f, o2) : f;
-  }
-  uint32_t fn = __shfl_down(f, 1, 64);
-  fn = (lane == 63 || fn > 63) ? 63u : fn;
+  // fn: the first lane after this one where a run stops passing through (63 if none)
+  const uint64_t above = ballot(!mid) & (~1ull << lane);
+  const uint32_t fn = above ? ctz64(above) : 63u;
   const uint32_t Cf = __shfl(Cs, fn, 64);
   const bool starts = trail > 0 && !mid;
   const uint32_t merged = starts ? trail + Cf - Cs : 0u;  // the run this lane's last run starts
@@ -511,6 +534,9 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   // ---- G. the lanes' tokens into the slot, then the slot to the writer ----
   uint8_t* const stg = S.ring[slot];
   if (!(SC_ABL & 1)) {
+    // the output bytes are or-ed into a zeroed slot: no masks, no branches per piece (the zeroes
+    // land first: a wave's LDS operations execute in order)
+    for (uint32_t u = lane; 16 * u < total; u += 64) reinterpret_cast<uint4*>(stg)[u] = make_uint4(0, 0, 0, 0);
     const uint32_t stga = lds_addr(stg);
     uint32_t at = incl - size, p = s;
 #pragma unroll
@@ -519,31 +545,28 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
         const uint32_t tv = tk.t[j];
         const uint32_t q = c0 + (tv >> 24), L = (tv >> 16) & 0xffu, off = tv & 0xffffu;
         const uint32_t run = q - p;  // < 16
-        if (run) {
-          const uint32_t ts = (j == 0 && cont) ? 0u : 1u;
-          sc_lds_put(stga + at, sc_prepend(sc_ld128(S.blk, p), (run - 1) << 2, ts), ts + run);
-          at += ts + run;
-        }
+        const uint32_t ts = (j == 0 && cont) ? 0u : 1u;
+        const uint32_t len = run ? ts + run : 0u;
+        sc_lds_or(stga + at, sc_trim(sc_prepend(sc_ld128(S.blk, p), (run - 1) << 2, ts), len));
+        at += len;
         if (L <= 64) {
           uint32_t cs;
-          const uint32_t cv = sc_copy_piece(off, L, cs);
-          sc_lds_put3(stg + at, cv, cs);
+          sc_lds_or3(stga + at, sc_copy_piece(off, L, cs));
           at += cs;
         } else {  // emit_copy! (internal.jl:306-329): 64-byte pieces while >= 68, a 60 if > 64, the rest
           uint32_t R = L;
           while (R >= 68) {
-            sc_lds_put3(stg + at, (2u + (63u << 2)) | (off << 8), 3);
+            sc_lds_or3(stga + at, (2u + (63u << 2)) | (off << 8));
             at += 3;
             R -= 64;
           }
           if (R > 64) {
-            sc_lds_put3(stg + at, (2u + (59u << 2)) | (off << 8), 3);
+            sc_lds_or3(stga + at, (2u + (59u << 2)) | (off << 8));
             at += 3;
             R -= 60;
           }
           uint32_t cs;
-          const uint32_t cv = sc_copy_piece(off, R, cs);
-          sc_lds_put3(stg + at, cv, cs);
+          sc_lds_or3(stga + at, sc_copy_piece(off, R, cs));
           at += cs;
         }
         p = q + L;
@@ -553,8 +576,8 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       const uint32_t run = ce - p;
       uint32_t tag = 0, ts = 0;
       if (!(tk.n == 0 && cont)) tag = sc_lit_tag(merged, ts);
-      sc_lds_put(stga + at, sc_prepend(sc_ld128(S.blk, p), tag, ts), min(ts + run, 16u));
-      if (ts + run > 16) sc_lds_put(stga + at + 16, sc_ld128(S.blk, p + 16 - ts), ts + run - 16);
+      sc_lds_or(stga + at, sc_trim(sc_prepend(sc_ld128(S.blk, p), tag, ts), min(ts + run, 16u)));
+      if (ts + run > 16) sc_lds_or(stga + at + 16, sc_trim(sc_ld128(S.blk, p + 16 - ts), ts + run - 16));
     }
   }
   // (a wave's LDS operations execute in order: the writer that sees the size sees the bytes)
