@@ -63,6 +63,12 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #ifndef SC_ABL
 #define SC_ABL 0
 #endif
+#ifndef SC_WPRIO
+#define SC_WPRIO 3
+#endif
+#ifndef SC_TPRIO
+#define SC_TPRIO 3
+#endif
 
 #if SM_STAMP
 __device__ unsigned long long g_stamp_sc[12];
@@ -287,6 +293,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   STAMP(0)
   STAMP_COUNT(11, 1)
   // ---- B. the insert token: 16 masked exchanges in position order, then hand it on ----
+  __builtin_amdgcn_s_setprio(SC_TPRIO);
   for (uint32_t it = 0; !(SC_ABL & 16) && uniform(__hip_atomic_load(&S.ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != k; ++it) {
     if (it > kScSpinMax) {  // never expected: a broken hand-off must not hang the GPU
       S.err |= 1;  // (the insert token)
@@ -627,11 +634,14 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, const 
                                                                uint8_t* const dst, uint32_t hv, uint32_t nsc,
                                                                uint32_t lane) {
   uint32_t o = hv, err = 0;
+  STAMP_DECL
   for (uint32_t k = 0; k < nsc; ++k) {
     const uint32_t slot = k % kScRing;
     const uint32_t sz = sc_wait(&S.rsize[slot], [](uint32_t v) { return v != 0; }, err, 4u) - 1;
+    STAMP(8)
     if (err) break;
     if (!(SC_ABL & 32)) sc_copy_out(dst + o, S.ring[slot], sz, lane);
+    STAMP(9)
     o += sz;
     // (this wave's slot reads are issued before these writes, and LDS runs them in order)
     __hip_atomic_store(&S.rsize[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -662,6 +672,7 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, const 
   }
   err |= uniform(__hip_atomic_load(&S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
   if (lane == 0) a.out_len[b] = err ? 0xfff00000u | err : o;  // (an error mark: > any block's length)
+  STAMP_FLUSH(g_stamp_sc)
 }
 
 // Persistent: one workgroup per CU walks blocks blockIdx.x, + gridDim.x, ...; each wave loads its
@@ -742,7 +753,9 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
 
     const uint32_t nsc = (n + kScS - 1) / kScS;
     if (wave == kScWorkers) {
+      __builtin_amdgcn_s_setprio(SC_WPRIO);  // (the writer's chain gates the slots)
       sc_writer(S, a, b, n, dst, hv, nsc, lane);
+      __builtin_amdgcn_s_setprio(0);
     } else {
       // (no lane-0-only code here or at the end of a super-chunk: the compiler merged two such
       // regions across the loop's back edge into a divergent loop that hung the wave)

@@ -15,14 +15,21 @@ namespace sm {
 #endif
 #if SM_STAMP
 #define STAMP_MACROS(NS) constexpr int kStampSlots = NS;
-#define STAMP_DECL                                \
-  uint64_t st_acc[kStampSlots] = {};              \
-  uint64_t st_t = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                      \
-  {                                                   \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
-    st_acc[i] += t_ - st_t;                           \
-    st_t = t_;                                        \
+// (s_memtime in volatile asm with a memory clobber: the builtin can be moved across the code it
+// is meant to bracket)
+__device__ inline uint64_t stamp_now() {
+  uint64_t t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
+  return t;
+}
+#define STAMP_DECL                   \
+  uint64_t st_acc[kStampSlots] = {}; \
+  uint64_t st_t = stamp_now();
+#define STAMP(i)                     \
+  {                                  \
+    const uint64_t t_ = stamp_now(); \
+    st_acc[i] += t_ - st_t;          \
+    st_t = t_;                       \
   }
 #define STAMP_COUNT(i, v) st_acc[i] += (v);
 #define STAMP_FLUSH(arr) \

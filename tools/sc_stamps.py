@@ -17,7 +17,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 NAMES = ["A hash", "B token wait", "B exchange", "C verify", "D walks+resync", "E sizes", "F base wait",
-         "G emission", "prologue (per wave)", "epilogue barrier (per wave)"]
+         "G emission", "writer: wait for a slot", "writer: copy-out"]
 
 
 def main():
@@ -42,11 +42,11 @@ def main():
     fn(buf, 1)
     v = list(buf)
     nsc = max(v[11], 1)
-    tot = sum(v[:10])
+    tot = sum(v[:8])
     print("data %s: %d super-chunks, %.2f resync iterations each" % (args.data, nsc, v[10] / nsc))
     for i, nme in enumerate(NAMES):
-        print("  %-28s %5.1f%%  %8.0f cycles/super-chunk" % (nme, 100.0 * v[i] / tot, v[i] / nsc))
-    print("  total                        %8.0f cycles/super-chunk (wave time)" % (tot / nsc))
+        print("  %-28s %5.1f%%  %8.0f cycles/super-chunk" % (nme, 100.0 * v[i] / tot if i < 8 else 0.0, v[i] / nsc))
+    print("  total (worker sections)      %8.0f cycles/super-chunk (wave time)" % (tot / nsc))
     print("roundtrip ok:", b.verify())
 
 
