@@ -301,9 +301,9 @@ def pmc_traffic(kernel):
 # the rocprof kernels behind each timed call (a fast-mode compress is the incompressible screen
 # then the parse; avg_launch_ms is their sum, HIP events around the call)
 ROCPROF_KERNELS = {
-    "compress_fast": ["sm::k_literal_screen", "sm::k_compress_fast<1>"],
-    "compress_fast_random": ["sm::k_literal_screen", "sm::k_compress_fast<1>"],
-    "compress_fragments": ["sm::k_literal_screen", "sm::k_compress_fast<1>"],
+    "compress_fast": ["sm::k_literal_screen", "sm::k_compress_sc<0>"],
+    "compress_fast_random": ["sm::k_literal_screen", "sm::k_compress_sc<0>"],
+    "compress_fragments": ["sm::k_literal_screen", "sm::k_compress_sc<0>"],
     "uncompress": ["sm::k_decompress"],
     "uncompress_random": ["sm::k_decompress"],
 }

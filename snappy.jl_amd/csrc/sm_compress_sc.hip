@@ -8,7 +8,8 @@
 // super-chunks whose copies stop at the super-chunk end.
 //
 // Persistent: one 16-wave workgroup per CU walks its blocks; the block (64 KiB) and a 32 KiB hash
-// table live in LDS.  A wave takes the next super-chunk of the block from an LDS counter and:
+// table live in LDS.  Each of 15 worker waves takes the next super-chunk of the block from an LDS
+// counter and:
 //  A. hashes its 16 groups of 64 positions (the reference's multiply, internal.jl:94, 13 bits);
 //  B. waits for the insert token, then ONE ds_mskor_rtn_b32 per group exchanges the positions into
 //     the table and hands the token on.  A table dword holds two u16 slots (position + 1): group
@@ -17,19 +18,22 @@
 //     a wave's LDS instructions execute in order, and the conflicting lanes of one instruction in
 //     ascending lane order) and the latest one of the other parity.  Correctness never depends on
 //     that order (every candidate is verified); only the ratio does;
-//  C. verifies both candidates (8 bytes, then 16 where both fill 8), keeps the longer, and stores
-//     per position the match length (u8; 1/2 = "extend from 8/16") and offset (u16), position-
-//     major so that a lane's 16 positions are one aligned 16-byte row, plus the match bitmask;
-//  D. each LANE loads its row into registers and walks its 16 positions greedily and serially (the
-//     reference's loop: literal runs skipped through the bitmask, a match extended 16 bytes a step
-//     up to 255 bytes).  A copy can end inside a later lane's positions, so the walks are
-//     resynchronised: every lane starts at its first position; a lane whose true start (the previous
-//     lane's end) differs walks from there until it lands on its old path, and keeps the old tokens
-//     from that point on; repeated until no start changes;
-//  E. literal runs that cross lanes get one tag (segmented scan), token sizes, a DPP scan;
-//  G1. the lanes write their tokens into an LDS staging buffer (masked ors: lanes share dwords);
-//  F. the super-chunk's output offset comes from the previous super-chunk (an LDS word), and
-//  G2. the wave copies the staging buffer out with aligned 16-byte stores.
+//  C. checks both candidates' first 4 bytes (the more recent first) and keeps the first that
+//     matches: per position its offset (u16, rows of 16 positions, swizzled) and the row's match
+//     bitmask.  No match length is computed here;
+//  D. each LANE walks its row's 16 positions greedily and serially (the reference's loop): at a
+//     match position it computes the match length (a 16-byte compare; the walk's last token is
+//     extended 16 bytes a step up to 255 bytes), records it, and jumps to the first match at or
+//     after the copy's end.  Only the positions a walk visits get a length (about a fifth).  A copy
+//     can end inside a later lane's positions, so the walks are resynchronised: every lane starts
+//     at its first position; a lane whose true start (the previous lane's end) differs walks from
+//     there until it lands on its old path, and keeps the old tokens from that point on; repeated
+//     until no start changes;
+//  E. literal runs that cross lanes get one tag (segmented by a ballot), token sizes, a DPP scan;
+//  F. the wave waits for its staging slot (super-chunk k takes slot k mod 8);
+//  G. the lanes or their tokens and literal bytes into the zeroed slot, and
+//  W. the writer wave (wave 15) copies the staged super-chunks out in order at the running output
+//     offset with aligned 16-byte stores, and writes the block's length.
 // Output is deterministic.
 #include "sm_device.h"
 #include "sm_internal.h"
@@ -86,7 +90,6 @@ struct ScLds {
   uint32_t T[kScTabWords + 4];         // hash table (two u16 slots a dword); T[kScTabWords] is the dummy for invalid lanes
   ScWaveLds w[kScWorkers];
   uint8_t ring[kScRing][kScSlot];      // staged outputs: super-chunk k in slot k % kScRing
-  uint64_t M[kScWorkers][kScG];        // per worker: match bitmask (bit = position of the super-chunk)
   uint32_t rsize[kScRing];             // the staged super-chunk's output size + 1 (0: slot not staged)
   uint32_t rseq[kScRing];              // the super-chunk a slot takes next (the writer frees it so)
   uint32_t ins;                        // insert token: super-chunks inserted so far
@@ -359,10 +362,15 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (m1 ? p1 : p2));
     mbs[g] = ballot(m1 || m2);
   }
-  if (lane == 0) {  // (one branch after the groups: a branch per group would stop their overlap)
-#pragma unroll
-    for (int g = 0; g < (int)kScG; ++g) S.M[wave][g] = mbs[g];
-  }
+  // the row masks: lane d holds dword d of the 16 group ballots (v_writelane), lane l reads its
+  // row's 16 bits from lane l / 2 (one ds_bpermute; no LDS array, no single-lane stores)
+  uint32_t mdw = 0;
+#define SC_WL(g)                                                                                  \
+  asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(mdw) : "s"((uint32_t)mbs[g]), "n"(2 * (g)));   \
+  asm volatile("v_writelane_b32 %0, %1, %2" : "+v"(mdw) : "s"((uint32_t)(mbs[g] >> 32)), "n"(2 * (g) + 1));
+  SC_WL(0) SC_WL(1) SC_WL(2) SC_WL(3) SC_WL(4) SC_WL(5) SC_WL(6) SC_WL(7)
+  SC_WL(8) SC_WL(9) SC_WL(10) SC_WL(11) SC_WL(12) SC_WL(13) SC_WL(14) SC_WL(15)
+#undef SC_WL
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
   STAMP(3)
 
@@ -372,7 +380,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   // jumps to the first match position at or after the copy's end (the row's match bitmask).
   const uint32_t c0 = sc0 + kScC * lane;
   const uint32_t ce = c0 < sce ? min(c0 + kScC, sce) : c0;
-  const uint32_t mask16 = reinterpret_cast<const uint16_t*>(S.M[wave])[lane];
+  const uint32_t mask16 = (__shfl(mdw, (int)(lane >> 1), 64) >> (16 * (lane & 1))) & 0xffffu;
   const uint32_t osw = (lane >> 2) & 7, lsw = (lane >> 3) & 3;  // the row's swizzles
   auto offAt = [&](uint32_t i) -> uint32_t { return Wl.O[16 * lane + 2 * ((i >> 1) ^ osw) + (i & 1)]; };
   uint8_t* const Lrow = Wl.L + 16 * lane;

@@ -20,7 +20,7 @@ def test_kernel_register_budgets(tmp_path):
     import re
     csrc = os.path.join(ROOT, "snappy.jl_amd", "csrc")
     usage = {}
-    for src in ("sm_compress_fast.hip", "sm_decompress.hip"):
+    for src in ("sm_compress_fast.hip", "sm_compress_sc.hip", "sm_decompress.hip"):
         out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fno-strict-aliasing",
                               "-fPIC", "-Rpass-analysis=kernel-resource-usage", "--cuda-device-only", "-c",
                               os.path.join(csrc, src), "-o", str(tmp_path / (src + ".o"))],
@@ -39,6 +39,12 @@ def test_kernel_register_budgets(tmp_path):
     assert len(fast) == 2, usage.keys()
     for k in fast:
         assert usage[k]["VGPRs"] < 128 and usage[k]["VGPRs Spill"] == 0, (k, usage[k])
+    # the shipped fast compressor (sm_compress_sc.hip): 16-wave workgroups, so at most 128 VGPRs;
+    # its only spill is the next block's 16 prefetch registers, stored and reloaded once per block
+    # (outside the super-chunk loop)
+    sc = [k for k in usage if "k_compress_sc" in k]
+    assert len(sc) == 1, usage.keys()
+    assert usage[sc[0]]["VGPRs"] <= 128 and usage[sc[0]]["VGPRs Spill"] <= 16, usage[sc[0]]
     dec = [k for k in usage if k.endswith("k_decompressENS_14DecompressArgsE")]
     assert dec and usage[dec[0]]["Occupancy [waves/SIMD]"] >= 7, usage.get(dec[0] if dec else None)
 

@@ -20,9 +20,9 @@ from pmc_summary import summarise  # noqa: E402
 # bench.py roofline key -> (pass directory, rocprof kernel names summed per launch).  A fast-mode
 # compress call is two kernels: the incompressible screen and the parse (which returns at once
 # for the blocks the screen emitted).
-KERNELS = {"compress_fast": ("pmc_compress", ["k_literal_screen", "k_compress_fast<1>"]),
+KERNELS = {"compress_fast": ("pmc_compress", ["k_literal_screen", "k_compress_sc<0>"]),
            "uncompress": ("pmc_uncompress", ["k_decompress("]),
-           "compress_fast_random": ("pmc_compress_random", ["k_literal_screen", "k_compress_fast<1>"]),
+           "compress_fast_random": ("pmc_compress_random", ["k_literal_screen", "k_compress_sc<0>"]),
            "uncompress_random": ("pmc_uncompress_random", ["k_decompress("])}
 IN_BYTES = 10000 * 65536  # uncompressed bytes per launch (tools/pmc_run.sh BLOCKS=10000)
 
