@@ -800,7 +800,7 @@ extern "C" int sm_debug_stamps_c(unsigned long long* out, int reset) {
 // hash range (the reference's multiply, internal.jl:94).  Repeated content repeats its anchors at
 // any distance, so a block counts the anchors whose word an earlier-inserted anchor already had
 // (an LDS table of 4 K words, exchanged).  Text and structured data count hundreds; random,
-// compressed and encrypted data count ~0.  The first 16 KiB go first (text decides there); the rest
+// compressed and encrypted data count ~0.  The first 8 KiB go first (text decides there); the rest
 // of the block is read only when they show no repeats.  Below kScrMin the block is emitted here as
 // ONE literal (header, emit_literal! tag, the bytes: internal.jl:271-284 -- the reference's own
 // output for random 64 KiB blocks is also one 65,542-B literal) from the registers that read it,
@@ -812,7 +812,7 @@ constexpr uint32_t kScrMin = 8;           // repeated anchors that make a block 
 constexpr uint32_t kScrMinLen = 8192;     // smaller blocks always take the parse
 constexpr uint32_t kScrThreads = 512;
 constexpr uint32_t kScrPieces = kBlockSize / 16 / kScrThreads;  // 16-B pieces per thread (8)
-constexpr uint32_t kScrFirst = 2;                               // pieces of the first pass (16 KiB)
+constexpr uint32_t kScrFirst = 1;                               // pieces of the first pass (8 KiB)
 constexpr uint32_t kScrTabBits = 12;
 constexpr uint32_t kScrEmpty = 0xffffffffu;  // its hash is no anchor, so no anchor word equals it
 static_assert(((kScrEmpty * kHashMul) >> 26) != 0, "the empty mark must not be an anchor word");
@@ -881,7 +881,7 @@ __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) 
     __syncthreads();
   };
   pass(0, kScrFirst, 0);
-  if (cnt[0] >= kScrMin) {  // text and structured data decide on their first 16 KiB
+  if (cnt[0] >= kScrMin) {  // text and structured data decide on their first 8 KiB
     if (tid == 0) a.out_len[b] = kScreenTodo;
     return;
   }

@@ -1,5 +1,5 @@
-"""The incompressible screen (k_literal_screen, sm_compress_fast.hip): blocks whose 4 KiB sample
-shows (almost) no repeated 4-grams are emitted as ONE literal -- header, emit_literal! tag
+"""The incompressible screen (k_literal_screen, sm_compress_fast.hip): blocks whose content-defined
+anchors (4-byte words hashing into the top 1/64) show (almost) no repeats are emitted as ONE literal -- header, emit_literal! tag
 (src/internal.jl:271-284), the bytes -- by an aligned 16-B byte-shifting copy.  These tests put
 that copy through every source/destination misalignment and ragged length, with and without the
 varint header (fragments), check the exact literal-only size, that nothing outside a block's
