@@ -964,7 +964,7 @@ hipError_t launch_compress_fast(const CompressArgs& a0, int mode, hipStream_t s)
     const char* v = getenv("SM_FAST_OLD");
     return v ? atoi(v) : 0;
   }();
-  if (!old) return launch_compress_sc(a, s);
+  if (!old) return launch_compress_sc(a, mode, s);
   return mode == 2 ? launch_depth<2>(a, s) : launch_depth<1>(a, s);
 }
 

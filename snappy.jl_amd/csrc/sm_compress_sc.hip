@@ -275,6 +275,7 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_next_block(const Co
 }
 
 // One super-chunk, by one wave (sections A-G2 above).
+template <int kDense>
 __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, const uint32_t k, const uint32_t n,
                                                                    const uint32_t wave, const uint32_t lane) {
   ScWaveLds& Wl = S.w[wave];
@@ -355,12 +356,29 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     // (c - 1 < q also rejects c == 0; the loads of a rejected candidate read the position itself)
     const bool ok1 = room && c1 - 1 < q, ok2 = room && c2 - 1 < q;
     const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
-    uint32_t v1 = lds_ld32(S.blk, p1), v2 = lds_ld32(S.blk, p2), w = lds_ld32(S.blk, q);
-    asm("" : "+v"(v1), "+v"(v2), "+v"(w));  // (keeps the loads unconditional)
-    const bool m1 = ok1 && v1 == w, m2 = ok2 && v2 == w;
     const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
-    Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (m1 ? p1 : p2));
-    mbs[g] = ballot(m1 || m2);
+    if constexpr (kDense) {
+      // dense mode: both candidates compared over 16 bytes, the longer kept (ties: the more
+      // recent), its length stored for the walks
+      const uint4 X = sc_ld128(S.blk, q);
+      uint32_t lw1 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p1 & ~3u)), p1 & 3u);
+      uint32_t lw2 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p2 & ~3u)), p2 & 3u);
+      asm("" : "+v"(lw1), "+v"(lw2));  // (keeps the loads unconditional)
+      const uint32_t l1 = ok1 ? lw1 : 0u, l2 = ok2 ? lw2 : 0u;
+      const bool take2 = l2 > l1;
+      const uint32_t l = take2 ? l2 : l1;
+      const uint32_t avail = sce - q;  // (>= 4 where l >= 4: room)
+      const uint32_t enc = l < 4 ? 0u : ((l == 16 && avail > 16) ? kScExt : min(l, avail));
+      Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (take2 ? p2 : p1));
+      Wl.L[16 * r4 + 4 * ((i >> 2) ^ ((g >> 1) & 3)) + (i & 3)] = (uint8_t)enc;
+      mbs[g] = ballot(l >= 4);
+    } else {
+      uint32_t v1 = lds_ld32(S.blk, p1), v2 = lds_ld32(S.blk, p2), w = lds_ld32(S.blk, q);
+      asm("" : "+v"(v1), "+v"(v2), "+v"(w));  // (keeps the loads unconditional)
+      const bool m1 = ok1 && v1 == w, m2 = ok2 && v2 == w;
+      Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (m1 ? p1 : p2));
+      mbs[g] = ballot(m1 || m2);
+    }
   }
   // the row masks: lane d holds dword d of the 16 group ballots (v_writelane), lane l reads its
   // row's 16 bits from lane l / 2 (one ds_bpermute; no LDS array, no single-lane stores)
@@ -403,13 +421,18 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
         } else {
           path |= 1u << i;
           last = i;
-          const uint32_t q = c0 + i, off = offAt(i);
-          const uint4 X = sc_ld128(S.blk, q);
-          const uint32_t p = q - off;
-          const uint32_t l = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p & ~3u)), p & 3u);
-          const uint32_t avail = sce - q;
-          const uint32_t enc = (l == 16 && avail > 16) ? kScExt : min(l, avail);
-          Lrow[4 * ((i >> 2) ^ lsw) + (i & 3)] = (uint8_t)enc;
+          uint32_t enc;
+          if constexpr (kDense) {
+            enc = Lrow[4 * ((i >> 2) ^ lsw) + (i & 3)];  // (computed in C)
+          } else {
+            const uint32_t q = c0 + i, off = offAt(i);
+            const uint4 X = sc_ld128(S.blk, q);
+            const uint32_t p = q - off;
+            const uint32_t l = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p & ~3u)), p & 3u);
+            const uint32_t avail = sce - q;
+            enc = (l == 16 && avail > 16) ? kScExt : min(l, avail);
+            Lrow[4 * ((i >> 2) ^ lsw) + (i & 3)] = (uint8_t)enc;
+          }
           lastL = enc;
           const uint32_t t = i + min(enc, 16u);  // <= 31: mask16 >> t is 0 past the row
           const uint32_t m = mask16 >> t;
@@ -686,7 +709,7 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, const 
 // Persistent: one workgroup per CU walks blocks blockIdx.x, + gridDim.x, ...; each wave loads its
 // share of the next block into registers as soon as it runs out of super-chunks, so the HBM
 // latency of the staging hides behind the block's tail.
-template <int kDummy>
+template <int kDense>
 __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
   __shared__ __attribute__((aligned(16))) ScLds S;
   const uint32_t tid = threadIdx.x;
@@ -771,7 +794,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
         // every lane adds 1 (one ds_add of 64 after the atomic optimizer); lane 0 sees a multiple of 64
         const uint32_t k = uniform(__hip_atomic_fetch_add(&S.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 6;
         if (k >= nsc) break;
-        sc_superchunk(S, k, n, wave, lane);
+        sc_superchunk<kDense>(S, k, n, wave, lane);
       }
     }
     SC_FETCH(bn)  // the next block's bytes, in flight behind the other waves' last super-chunks
@@ -792,7 +815,9 @@ extern "C" int sm_debug_stamps_sc(unsigned long long* out, int reset) {
 }
 #endif
 
-hipError_t launch_compress_sc(const CompressArgs& a, hipStream_t s) {
+// mode 1 (SM_MODE_FAST): the more recent 4-byte match per position; mode 2 (SM_MODE_FAST_DENSE): the
+// longer of the two candidates over 16 bytes (smaller output, about 15% slower)
+hipError_t launch_compress_sc(const CompressArgs& a, int mode, hipStream_t s) {
   static uint32_t ncu_cache[64] = {};
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
@@ -804,7 +829,10 @@ hipError_t launch_compress_sc(const CompressArgs& a, hipStream_t s) {
     __atomic_store_n(&ncu_cache[dev], ncu, __ATOMIC_RELAXED);
   }
   const uint32_t grid = min(a.nblk, ncu);  // one workgroup per CU (the LDS holds one)
-  hipLaunchKernelGGL(k_compress_sc<0>, dim3(grid), dim3(kScThreads), 0, s, a);
+  if (mode == 2)
+    hipLaunchKernelGGL(k_compress_sc<1>, dim3(grid), dim3(kScThreads), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_compress_sc<0>, dim3(grid), dim3(kScThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -37,7 +37,7 @@ struct DecompressArgs {
 // mode 0 = reference (byte-identical to Snappy.jl), 1 = fast (wave-parallel parse), 2 = fast, denser
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s);
 hipError_t launch_compress_fast(const CompressArgs& a, int mode, hipStream_t s);
-hipError_t launch_compress_sc(const CompressArgs& a, hipStream_t s);  // sm_compress_sc.hip (after the screen)
+hipError_t launch_compress_sc(const CompressArgs& a, int mode, hipStream_t s);  // sm_compress_sc.hip (after the screen)
 hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 
 // One large stream decoded in parallel (sm_uncompress): an index pass over 4 KiB chunks of the

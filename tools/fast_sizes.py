@@ -13,18 +13,20 @@ import oracle as O  # noqa: E402
 def main():
     sm = bench.load_package()
     tdir = os.path.join(ROOT, "tests", "golden", "testdata")
-    worst = 0.0
+    worst = worstd = 0.0
     for f in sorted(os.listdir(tdir)):
         if f.endswith(".snappy") or f.startswith("baddata"):
             continue
         raw = open(os.path.join(tdir, f), "rb").read()
         ref = len(O.compress(raw))
         fast = sm.compress(raw, mode="fast")
-        assert O.uncompress(fast) == raw
-        r = len(fast) / ref
+        dense = sm.compress(raw, mode="dense")
+        assert O.uncompress(fast) == raw and O.uncompress(dense) == raw
+        r, rd = len(fast) / ref, len(dense) / ref
         worst = max(worst, r)
-        print("%-20s %9d  ref %9d  fast %9d  fast/ref %.4f" % (f, len(raw), ref, len(fast), r))
-    print("worst fast/ref %.4f" % worst)
+        worstd = max(worstd, rd)
+        print("%-20s %9d  ref %9d  fast %9d (%.4f)  dense %9d (%.4f)" % (f, len(raw), ref, len(fast), r, len(dense), rd))
+    print("worst fast/ref %.4f, dense/ref %.4f" % (worst, worstd))
 
 
 if __name__ == "__main__":
