@@ -277,7 +277,11 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_next_block(const Co
 // One super-chunk, by one wave (sections A-G2 above).
 template <int kDense>
 __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, const uint32_t k, const uint32_t n,
-                                                                   const uint32_t wave, const uint32_t lane) {
+                                                                   const uint32_t wave, const uint32_t lane_in) {
+  // (the lane index laundered per super-chunk: otherwise the compiler hoists dozens of lane-derived
+  // addresses out of the super-chunk loop, and the registers they hold serialise section C)
+  uint32_t lane = lane_in;
+  asm volatile("" : "+v"(lane));
   ScWaveLds& Wl = S.w[wave];
   const uint32_t sc0 = k * kScS, sce = min(sc0 + kScS, n);
   const uint32_t Tbase = lds_addr(S.T);
