@@ -6,7 +6,7 @@ mkdir -p $O
 for rep in 1 2; do
   for L in default "$@"; do
     if [ "$L" = default ]; then unset SNAPPY_MI355X_LIB; else export SNAPPY_MI355X_LIB=$L; fi
-    timeout -k 10 120 python3 tools/kbench.py --op compress_fast --blocks 10000 --reps 20 > $O/k.log 2>&1 || { echo "$L failed"; tail $O/k.log; exit 1; }
+    timeout -k 10 120 python3 tools/kbench.py --op ${OP:-compress_fast} --blocks 10000 --reps 20 > $O/k.log 2>&1 || { echo "$L failed"; tail $O/k.log; exit 1; }
     echo "$L: $(grep -v amdgpu.ids $O/k.log | tr '\n' ' ')"
   done
 done
