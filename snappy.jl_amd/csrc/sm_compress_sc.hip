@@ -213,11 +213,17 @@ __device__ inline uint32_t sc_lit_tag(uint32_t len, uint32_t& sz) {
   return sz == 1 ? (l1 << 2) : (sz == 2 ? (60u << 2) | (l1 << 8) : (61u << 2) | (l1 << 8));
 }
 
+// c ? a : b on values (a conditional on lvalues can become a select of their addresses)
+__device__ inline uint32_t sc_sel(uint32_t c, uint32_t a, uint32_t b) { return c ? a : b; }
+
 // one emit_copy_upto_64! piece (internal.jl:289-304), L in 4..64: copy-1 or copy-2, and its size
 __device__ inline uint32_t sc_copy_piece(uint32_t off, uint32_t L, uint32_t& sz) {
   const bool c1 = L < 12 && off < 2048;
   sz = c1 ? 2u : 3u;
-  return c1 ? (1u + ((L - 4) << 2) + ((off >> 3) & 0xe0u)) | ((off & 0xffu) << 8) : (2u + ((L - 1) << 2)) | (off << 8);
+  // (both encodings, then a select: the compiler otherwise branches on c1)
+  const uint32_t e1 = (1u + ((L - 4) << 2) + ((off >> 3) & 0xe0u)) | ((off & 0xffu) << 8);
+  const uint32_t e2 = (2u + ((L - 1) << 2)) | (off << 8);
+  return sc_sel(c1, e1, e2);
 }
 
 __device__ inline uint32_t sc_extend(const uint8_t* blk, uint32_t q, uint32_t off, uint32_t L, uint32_t cap) {
@@ -228,6 +234,16 @@ __device__ inline uint32_t sc_extend(const uint8_t* blk, uint32_t q, uint32_t of
     L = min(L + fb, cap);
     if (fb < 16 || L >= cap) return L;
   }
+}
+
+// copy_tag_bytes (emit_copy!, internal.jl:306-329) for 4 <= L <= 255 in closed form: k 64-byte
+// pieces while L >= 68, a 60-byte piece if more than 64 remain, then one piece of <= 64
+__device__ inline uint32_t sc_copy_bytes(uint32_t off, uint32_t L) {
+  const uint32_t k = L >= 68 ? (L - 4) >> 6 : 0u;
+  const uint32_t R0 = L - 64 * k;
+  const uint32_t x = R0 > 64 ? 1u : 0u;
+  const uint32_t R = R0 - 60 * x;
+  return 3 * (k + x) + ((R < 12 && off < 2048) ? 2u : 3u);
 }
 
 // lowest set bit of x, ~0 for 0 (v_ffbl_b32)
@@ -249,8 +265,6 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_eq16(uint32_t X0, u
   return min(min(b0, b1), min(min(b2, b3), 128u)) >> 3;
 }
 
-// c ? a : b on values (a conditional on lvalues can become a select of their addresses)
-__device__ inline uint32_t sc_sel(uint32_t c, uint32_t a, uint32_t b) { return c ? a : b; }
 
 // bits [a, b) of a u32 (0 <= a <= b <= 31)
 __device__ inline uint32_t sc_bits(uint32_t a, uint32_t b) { return ((1u << b) - 1u) & ~((1u << a) - 1u); }
@@ -287,11 +301,12 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   const uint32_t Tbase = lds_addr(S.T);
   STAMP_DECL
   // ---- A. hashes of the 16 groups: LDS byte address of the bucket dword, the slot value ----
-  uint32_t ha[kScG], hvv[kScG];
+  uint32_t ha[kScG], hvv[kScG], wq[kScG];
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
     const uint32_t q = sc0 + 64 * g + lane;
     const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, (q & ~3u) + 4), sc_ld32(S.blk, q & ~3u), q & 3u);
+    wq[g] = w;
     const uint32_t h = (w * kHashMul) >> (32 - kScTabBits);
     const bool valid = q + 4 <= n;
     ha[g] = Tbase + 4 * (valid ? h : kScTabWords);
@@ -377,8 +392,9 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       Wl.L[16 * r4 + 4 * ((i >> 2) ^ ((g >> 1) & 3)) + (i & 3)] = (uint8_t)enc;
       mbs[g] = ballot(l >= 4);
     } else {
-      uint32_t v1 = lds_ld32(S.blk, p1), v2 = lds_ld32(S.blk, p2), w = lds_ld32(S.blk, q);
-      asm("" : "+v"(v1), "+v"(v2), "+v"(w));  // (keeps the loads unconditional)
+      uint32_t v1 = lds_ld32(S.blk, p1), v2 = lds_ld32(S.blk, p2);
+      const uint32_t w = wq[g];
+      asm("" : "+v"(v1), "+v"(v2));  // (keeps the loads unconditional)
       const bool m1 = ok1 && v1 == w, m2 = ok2 && v2 == w;
       Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (m1 ? p1 : p2));
       mbs[g] = ballot(m1 || m2);
@@ -526,25 +542,22 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   // lead == trail); body: every other byte of the lane's output
   const bool live = s >= c0 && s < ce;
   uint32_t lead = 0, body = 0, trail = 0;
-  {
+  {  // (selects, no branches: every lane runs all four token slots)
     uint32_t p = s;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      if ((uint32_t)j < tk.n) {
-        const uint32_t tv = tk.t[j];
-        const uint32_t q = c0 + (tv >> 24), L = (tv >> 16) & 0xffu, run = q - p;
-        if (j == 0)
-          lead = run;
-        else if (run)
-          body += run + 1;  // an internal run (< 16 bytes: a one-byte tag)
-        body += copy_tag_bytes(tv & 0xffffu, L);
-        p = q + L;
-      }
+      const bool has = (uint32_t)j < tk.n;
+      const uint32_t tv = tk.t[j];
+      const uint32_t q = c0 + (tv >> 24), L = (tv >> 16) & 0xffu, run = q - p;
+      if (j == 0)
+        lead = sc_sel(has, run, 0u);
+      else
+        body += sc_sel(has && run, run + 1, 0u);  // an internal run (< 16 bytes: a one-byte tag)
+      body += sc_sel(has, sc_copy_bytes(tv & 0xffffu, L), 0u);
+      p = sc_sel(has, q + L, p);
     }
-    if (live && p < ce) {
-      trail = ce - p;
-      if (tk.n == 0) lead = trail;
-    }
+    trail = (live && p < ce) ? ce - p : 0u;
+    lead = tk.n == 0 ? trail : lead;
   }
   const uint32_t ptrail = __builtin_amdgcn_update_dpp(0u, trail, 0x138, 0xf, 0xf, false);  // wave_shr:1 (lane 0: 0)
   const bool cont = ptrail > 0 && lead > 0;  // this lane's first run continues the previous lane's last one

