@@ -419,8 +419,11 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   const uint32_t c0 = sc0 + kScC * lane;
   const uint32_t ce = c0 < sce ? min(c0 + kScC, sce) : c0;
   const uint32_t mask16 = (__shfl(mdw, (int)(lane >> 1), 64) >> (16 * (lane & 1))) & 0xffffu;
-  const uint32_t osw = (lane >> 2) & 7, lsw = (lane >> 3) & 3;  // the row's swizzles
-  auto offAt = [&](uint32_t i) -> uint32_t { return Wl.O[16 * lane + 2 * ((i >> 1) ^ osw) + (i & 1)]; };
+  // the row's swizzles as index XORs: entry i of the row is u16 i ^ osw2 of the O row and byte
+  // i ^ lsw4 of the L row (2 ((i >> 1) ^ osw) + (i & 1) = i ^ 2 osw; likewise for L)
+  const uint32_t osw2 = ((lane >> 2) & 7) << 1, lsw4 = ((lane >> 3) & 3) << 2;
+  const uint16_t* const Orow = Wl.O + 16 * lane;
+  auto offAt = [&](uint32_t i) -> uint32_t { return Orow[i ^ osw2]; };
   uint8_t* const Lrow = Wl.L + 16 * lane;
   // the last token's extended length (one per lane: resync walks often end on the same token)
   uint32_t xpos = 16, xlen = 0;
@@ -443,7 +446,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
           last = i;
           uint32_t enc;
           if constexpr (kDense) {
-            enc = Lrow[4 * ((i >> 2) ^ lsw) + (i & 3)];  // (computed in C)
+            enc = Lrow[i ^ lsw4];  // (computed in C)
           } else {
             const uint32_t q = c0 + i, off = offAt(i);
             const uint4 X = sc_ld128(S.blk, q);
@@ -451,7 +454,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
             const uint32_t l = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p & ~3u)), p & 3u);
             const uint32_t avail = sce - q;
             enc = (l == 16 && avail > 16) ? kScExt : min(l, avail);
-            Lrow[4 * ((i >> 2) ^ lsw) + (i & 3)] = (uint8_t)enc;
+            Lrow[i ^ lsw4] = (uint8_t)enc;
           }
           lastL = enc;
           const uint32_t t = i + min(enc, 16u);  // <= 31: mask16 >> t is 0 past the row
@@ -509,17 +512,8 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       }
     }
   }
-  // the lengths the walks recorded (every token of P has one)
-  uint32_t l0, l1, l2, l3;
-  {
-    const uint4 v = reinterpret_cast<const uint4*>(Wl.L)[lane];
-    l0 = v.x, l1 = v.y, l2 = v.z, l3 = v.w;
-  }
-  auto getL = [&](uint32_t i) -> uint32_t {
-    const uint32_t k = (i >> 2) ^ lsw;
-    const uint32_t d = sc_sel(k & 2, sc_sel(k & 1, l3, l2), sc_sel(k & 1, l1, l0));
-    return (d >> (8 * (i & 3))) & 0xffu;
-  };
+  // the lengths the walks recorded (every token of P has one), read back per token
+  auto getL = [&](uint32_t i) -> uint32_t { return Lrow[i ^ lsw4]; };
   // the lane's tokens from its token bits: offset | length << 16 | position-in-row << 24
   ScToks tk;
   {
