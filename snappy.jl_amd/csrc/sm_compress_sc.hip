@@ -73,6 +73,12 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #ifndef SC_TPRIO
 #define SC_TPRIO 3
 #endif
+#ifndef SC_TSLEEP  // s_sleep units (64 cycles) between polls of the insert token
+#define SC_TSLEEP 1
+#endif
+#ifndef SC_WSLEEP  // ... and of a staging slot's hand-off words
+#define SC_WSLEEP 1
+#endif
 
 #if SM_STAMP
 __device__ unsigned long long g_stamp_sc[12];
@@ -109,7 +115,7 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_wait(uint32_t* p, P
       err |= code;
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (SC_WSLEEP) __builtin_amdgcn_s_sleep(SC_WSLEEP);
   }
   return v;
 }
@@ -322,7 +328,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       S.err |= 1;  // (the insert token)
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    if (SC_TSLEEP) __builtin_amdgcn_s_sleep(SC_TSLEEP);
   }
   STAMP(1)
   __builtin_amdgcn_s_setprio(3);
