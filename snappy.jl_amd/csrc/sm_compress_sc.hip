@@ -378,8 +378,11 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
     const uint32_t c1 = (SC_ABL & 8) ? 0u : max(ca, cb), c2 = (SC_ABL & 8) ? 0u : min(ca, cb);
     const bool room = q + 4 <= sce;  // a match may cover 4 bytes before the super-chunk end
-    // (c - 1 < q also rejects c == 0; the loads of a rejected candidate read the position itself)
-    const bool ok1 = room && c1 - 1 < q, ok2 = room && c2 - 1 < q;
+    // A nonzero candidate is always an earlier position: the table is cleared per block and
+    // filled in position order (the own slot by lower lanes of the same instruction or earlier
+    // groups, the other slot by earlier groups), and lanes without room exchange into the dummy
+    // word.  The loads of a rejected candidate read the position itself.
+    const bool ok1 = room && c1 != 0, ok2 = room && c2 != 0;
     const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
     const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
     if constexpr (kDense) {
@@ -602,7 +605,8 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
         const uint32_t run = q - p;  // < 16
         const uint32_t ts = (j == 0 && cont) ? 0u : 1u;
         const uint32_t len = run ? ts + run : 0u;
-        sc_lds_or(stga + at, sc_trim(sc_prepend(sc_ld128(S.blk, p), (run - 1) << 2, ts), len));
+        if (ballot(len != 0))  // (uniform: skipped when no lane has a run before this token)
+          sc_lds_or(stga + at, sc_trim(sc_prepend(sc_ld128(S.blk, p), (run - 1) << 2, ts), len));
         at += len;
         if (L <= 64) {
           uint32_t cs;
