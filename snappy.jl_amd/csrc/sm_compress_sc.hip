@@ -67,6 +67,9 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #ifndef SC_ABL
 #define SC_ABL 0
 #endif
+#ifndef SC_FAR  // fast mode: the older of two matching candidates when the recent one is nearer
+#define SC_FAR 256
+#endif
 #ifndef SC_WPRIO
 #define SC_WPRIO 3
 #endif
@@ -405,7 +408,11 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       const uint32_t w = wq[g];
       asm("" : "+v"(v1), "+v"(v2));  // (keeps the loads unconditional)
       const bool m1 = ok1 && v1 == w, m2 = ok2 && v2 == w;
-      Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (m1 ? p1 : p2));
+      // the older candidate when the more recent one is nearer than SC_FAR bytes: a copy whose
+      // source is that close often reads the output of the decoder's own batch of tags, which
+      // then runs it in order
+      const bool use2 = m2 && (!m1 || q - p1 < (uint32_t)SC_FAR);
+      Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (use2 ? p2 : p1));
       mbs[g] = ballot(m1 || m2);
     }
   }

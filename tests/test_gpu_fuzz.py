@@ -1,6 +1,6 @@
 """Randomised round trips of the fast compressor on the GPU: structured blocks of ragged sizes
 (periodic patterns, runs, small alphabets, mutated text, random tails, planted copies at
-random distances) through fast and dense mode, decoded on the GPU and compared byte-for-byte,
+random distances, long repeats whose copies run to the 255-byte token cap across many rows) through fast and dense mode, decoded on the GPU and compared byte-for-byte,
 and every stream decoded by the CPU oracle (the reference's decoder restated) as well.  Fast mode
 has no byte-parity target: validity under the reference's decoder is the bar."""
 import os
@@ -17,7 +17,7 @@ SLOT = 76490 + 8  # sm_max_compressed_length(65536) + slack
 
 def gen_block(rng, text):
     n = int(rng.choice([rng.integers(1, 300), rng.integers(300, 65537), 65536]))
-    kind = int(rng.integers(0, 6))
+    kind = int(rng.integers(0, 8))
     if kind == 0:  # periodic pattern, random period
         b = np.resize(rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8), n)
     elif kind == 1:  # runs of random bytes and lengths
@@ -39,6 +39,16 @@ def gen_block(rng, text):
         b = text[s:s + n].copy()
         cut = int(rng.integers(0, b.size + 1))
         b[cut:] = rng.integers(0, 256, b.size - cut, dtype=np.uint8)
+    elif kind == 6:  # a random segment repeated, sparsely mutated: long extended copies
+        seg = rng.integers(0, 256, int(rng.integers(17, 5000)), dtype=np.uint8)
+        b = np.resize(seg, n).copy()
+        m = rng.random(b.size) < rng.choice([0.0, 0.0005, 0.005])
+        b[m] = rng.integers(0, 256, int(m.sum()), dtype=np.uint8)
+    elif kind == 7:  # a text segment repeated 2-4 times (html_x_4-like)
+        k = int(rng.integers(2, 5))
+        L = max(1, n // k)
+        s = int(rng.integers(0, max(1, text.size - L)))
+        b = np.resize(text[s:s + L], n).copy()
     else:  # random bytes with planted copies (long and overlapping matches)
         b = rng.integers(0, 256, n, dtype=np.uint8)
         for _ in range(int(rng.integers(1, 40))):
