@@ -237,20 +237,23 @@ __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt,
   }
   if (lane < kWalkLevels) jt[lane * kJtRow + 256] = 256;  // every row maps 256 to itself
   *reinterpret_cast<uint2*>(jt + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+  // The J_k are powers of J0, so they commute: lane t applies J_k for bit k of t as soon as row k
+  // is built, its read issued with the next row's reads (the chain does not wait for every row)
+  uint32_t c = 0;
 #pragma unroll
   for (int k = 1; k < kWalkLevels; ++k) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     const uint16_t* prev = jt + (k - 1) * kJtRow;
+    const uint32_t t = prev[c];
 #pragma unroll
     for (int j = 0; j < 4; ++j) J[j] = prev[J[j]];
+    c = ((lane >> (k - 1)) & 1u) ? t : c;
     *reinterpret_cast<uint2*>(jt + k * kJtRow + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
   }
   __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the u16 reads below follow the uint2 stores
-  uint32_t c = 0;
-#pragma unroll
-  for (int k = 0; k < kWalkLevels; ++k) {
-    const uint32_t t = jt[k * kJtRow + c];
-    c = ((lane >> k) & 1u) ? t : c;
+  {
+    const uint32_t t = jt[(kWalkLevels - 1) * kJtRow + c];
+    c = ((lane >> (kWalkLevels - 1)) & 1u) ? t : c;
   }
   if (lane >= 32) {  // J5 = J4 o J4
     const uint16_t* j4 = jt + (kWalkLevels - 1) * kJtRow;
