@@ -18,9 +18,10 @@
 //     a wave's LDS instructions execute in order, and the conflicting lanes of one instruction in
 //     ascending lane order) and the latest one of the other parity.  Correctness never depends on
 //     that order (every candidate is verified); only the ratio does;
-//  C. checks both candidates' first 4 bytes (the more recent first) and keeps the first that
-//     matches: per position its offset (u16, rows of 16 positions, swizzled) and the row's match
-//     bitmask.  No match length is computed here;
+//  C. checks both candidates' first 4 bytes and keeps the more recent one that matches, or the
+//     older one when the recent one is nearer than SC_FAR (256) bytes and the older matches too
+//     (fewer copies that read the decoder's own tag batch): per position its offset (u16, rows of
+//     16 positions, swizzled) and the row's match bitmask.  No match length is computed here;
 //  D. each LANE walks its row's 16 positions greedily and serially (the reference's loop): at a
 //     match position it computes the match length (a 16-byte compare; the walk's last token is
 //     extended 16 bytes a step up to 255 bytes), records it, and jumps to the first match at or
@@ -410,7 +411,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       const bool m1 = ok1 && v1 == w, m2 = ok2 && v2 == w;
       // the older candidate when the more recent one is nearer than SC_FAR bytes: a copy whose
       // source is that close often reads the output of the decoder's own batch of tags, which
-      // then runs it in order
+      // then runs it in order ("Candidates for the decoder")
       const bool use2 = m2 && (!m1 || q - p1 < (uint32_t)SC_FAR);
       Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (use2 ? p2 : p1));
       mbs[g] = ballot(m1 || m2);
