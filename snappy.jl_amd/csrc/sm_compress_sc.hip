@@ -311,16 +311,23 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   const uint32_t Tbase = lds_addr(S.T);
   STAMP_DECL
   // ---- A. hashes of the 16 groups: LDS byte address of the bucket dword, the slot value ----
+  // (group g's position is ql + 64 g: its dword address and byte shift are ql's plus a constant,
+  // so the loads take immediate offsets; only the block's last super-chunk has positions whose 4
+  // bytes run past the block, and only it checks them)
   uint32_t ha[kScG], hvv[kScG], wq[kScG];
+  const uint32_t ql = sc0 + lane, qa = ql & ~3u, qb = ql & 3u;
+  const uint32_t hv0 = ql + 1, hv1 = (ql + 1) << 16;
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
-    const uint32_t q = sc0 + 64 * g + lane;
-    const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, (q & ~3u) + 4), sc_ld32(S.blk, q & ~3u), q & 3u);
+    const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, qa + 64 * g + 4), sc_ld32(S.blk, qa + 64 * g), qb);
     wq[g] = w;
-    const uint32_t h = (w * kHashMul) >> (32 - kScTabBits);
-    const bool valid = q + 4 <= n;
-    ha[g] = Tbase + 4 * (valid ? h : kScTabWords);
-    hvv[g] = (q + 1) << (16 * (g & 1));
+    ha[g] = Tbase + 4 * ((w * kHashMul) >> (32 - kScTabBits));
+    hvv[g] = (g & 1) ? hv1 + ((64u * g) << 16) : hv0 + 64u * g;
+  }
+  if (sc0 + kScS + 3 > n) {  // (uniform) positions without 4 bytes exchange into the dummy word
+    asm volatile("");         // (a real branch: the selects are not speculated into every super-chunk)
+#pragma unroll
+    for (int g = 0; g < (int)kScG; ++g) ha[g] = ql + 64 * g + 4 <= n ? ha[g] : Tbase + 4 * kScTabWords;
   }
   const uint32_t mk0 = 0xffffu, mk1 = 0xffff0000u;
   STAMP(0)
@@ -381,12 +388,13 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t sh = 16 * (g & 1);
     const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
     const uint32_t c1 = (SC_ABL & 8) ? 0u : max(ca, cb), c2 = (SC_ABL & 8) ? 0u : min(ca, cb);
-    const bool room = q + 4 <= sce;  // a match may cover 4 bytes before the super-chunk end
     // A nonzero candidate is always an earlier position: the table is cleared per block and
     // filled in position order (the own slot by lower lanes of the same instruction or earlier
-    // groups, the other slot by earlier groups), and lanes without room exchange into the dummy
-    // word.  The loads of a rejected candidate read the position itself.
-    const bool ok1 = room && c1 != 0, ok2 = room && c2 != 0;
+    // groups, the other slot by earlier groups).  Positions without 4 bytes before the block end
+    // exchanged with the dummy word, and positions without 4 bytes before the super-chunk end may
+    // not start a copy: the walks' row masks leave both out (D), so no per-group check here.  The
+    // loads of a rejected candidate read the position itself.
+    const bool ok1 = c1 != 0, ok2 = c2 != 0;
     const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
     const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
     if constexpr (kDense) {
@@ -435,7 +443,9 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   // jumps to the first match position at or after the copy's end (the row's match bitmask).
   const uint32_t c0 = sc0 + kScC * lane;
   const uint32_t ce = c0 < sce ? min(c0 + kScC, sce) : c0;
-  const uint32_t mask16 = (__shfl(mdw, (int)(lane >> 1), 64) >> (16 * (lane & 1))) & 0xffffu;
+  // (a match may cover 4 bytes before the super-chunk end: positions c0 + i with c0 + i + 4 <= sce)
+  const uint32_t nroom = c0 + 3 < sce ? min(sce - c0 - 3, 16u) : 0u;
+  const uint32_t mask16 = (__shfl(mdw, (int)(lane >> 1), 64) >> (16 * (lane & 1))) & ((1u << nroom) - 1u);
   // the row's swizzles as index XORs: entry i of the row is u16 i ^ osw2 of the O row and byte
   // i ^ lsw4 of the L row (2 ((i >> 1) ^ osw) + (i & 1) = i ^ 2 osw; likewise for L)
   const uint32_t osw2 = ((lane >> 2) & 7) << 1, lsw4 = ((lane >> 3) & 3) << 2;
