@@ -190,12 +190,14 @@ __device__ inline uint4 sc_trim(uint4 v, uint32_t len) {
 // ors the 16 bytes v (zero past the piece) into the zeroed LDS byte array at byte address a (any
 // alignment): five ds_or_b32, unconditionally (an or of zeros leaves a neighbour's bytes alone)
 __device__ inline void sc_lds_or(uint32_t a, uint4 v) {
-  const uint32_t sh = a & 3u, wa = a & ~3u, r = 4 - sh;  // alignbyte(hi, lo, r) = (hi:lo) >> 8r
-  const uint32_t u0 = v.x << (8 * sh);
-  const uint32_t u1 = sh ? __builtin_amdgcn_alignbyte(v.y, v.x, r) : v.y;
-  const uint32_t u2 = sh ? __builtin_amdgcn_alignbyte(v.z, v.y, r) : v.z;
-  const uint32_t u3 = sh ? __builtin_amdgcn_alignbyte(v.w, v.z, r) : v.w;
-  const uint32_t u4 = sh ? v.w >> (8 * r) : 0u;
+  // the five dwords from (a - 1) & ~3: alignbyte(hi, lo, t) = (hi:lo) >> 8 (t & 3) with t = 4 - (a & 3),
+  // so an aligned a (t = 0) shifts the whole piece one dword up and or-s a zero below it (no selects)
+  const uint32_t wa = (a - 1u) & ~3u, t = (0u - a) & 3u;
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(v.x, 0u, t);
+  const uint32_t u1 = __builtin_amdgcn_alignbyte(v.y, v.x, t);
+  const uint32_t u2 = __builtin_amdgcn_alignbyte(v.z, v.y, t);
+  const uint32_t u3 = __builtin_amdgcn_alignbyte(v.w, v.z, t);
+  const uint32_t u4 = __builtin_amdgcn_alignbyte(0u, v.w, t);
   asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4\nds_or_b32 %0, %3 offset:8\nds_or_b32 %0, %4 offset:12\n"
                "ds_or_b32 %0, %5 offset:16"
                : : "v"(wa), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4) : "memory");
@@ -203,8 +205,8 @@ __device__ inline void sc_lds_or(uint32_t a, uint4 v) {
 
 // ors the (up to 3) bytes of cv into the zeroed LDS byte array at byte address a
 __device__ inline void sc_lds_or3(uint32_t a, uint32_t cv) {
-  const uint32_t sh = a & 3u, wa = a & ~3u;
-  const uint32_t lo = cv << (8 * sh), hi = sh ? cv >> (8 * (4 - sh)) : 0u;
+  const uint32_t wa = (a - 1u) & ~3u, t = (0u - a) & 3u;  // (as sc_lds_or)
+  const uint32_t lo = __builtin_amdgcn_alignbyte(cv, 0u, t), hi = __builtin_amdgcn_alignbyte(0u, cv, t);
   asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
 }
 
