@@ -96,6 +96,7 @@ struct ScWaveLds {
   uint16_t O[kScS];  // candidate offset per position, rows of 16, dword pairs swizzled by (row >> 2) & 7
 };
 struct ScLds {
+  uint8_t pre[16];                     // (read as the byte before position 0, then replaced by a tag)
   uint8_t blk[kBlockSize + 64];        // the block (+ pad: reads run up to 20 bytes past a position)
   uint32_t T[kScTabWords + 4];         // hash table (two u16 slots a dword); T[kScTabWords] is the dummy for invalid lanes
   ScWaveLds w[kScWorkers];
@@ -625,8 +626,14 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
         const uint32_t run = q - p;  // < 16
         const uint32_t ts = (j == 0 && cont) ? 0u : 1u;
         const uint32_t len = run ? ts + run : 0u;
-        if (ballot(len != 0))  // (uniform: skipped when no lane has a run before this token)
-          sc_lds_or(stga + at, sc_trim(sc_prepend(sc_ld128(S.blk, p), (run - 1) << 2, ts), len));
+        if (ballot(len != 0)) {  // (uniform: skipped when no lane has a run before this token)
+          // the run with the byte before it: the tag replaces that byte (ts = 1), or (ts = 0: the
+          // run continues the previous lane's, which ends on that very byte) it is or-ed again
+          // onto itself one byte early -- no prepend shifts
+          uint4 v = sc_ld128(S.blk - 4, p + 3);  // bytes from position p - 1
+          v.x = ts ? ((v.x & ~0xffu) | ((run - 1) << 2)) : v.x;
+          sc_lds_or(stga + at + ts - 1u, sc_trim(v, run ? run + 1 : 0u));
+        }
         at += len;
         if (L <= 64) {
           uint32_t cs;
