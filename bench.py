@@ -233,7 +233,9 @@ class StreamShard:
         self.uncompress(sm)
         ok = bool(torch.equal(self.d_dec[: self.in_bytes], self.d_in)) and int(self.status.abs().sum()) == 0
         ok = ok and bool((self.dec_len == self.in_len).all())
-        # the global index: offsets strictly increasing by this rank's sizes
+        # the global index: a real stream length (not poisoned by an error mark, dist.py), and
+        # offsets strictly increasing by this rank's sizes
+        ok = ok and self.stream_len is not None and int(self.stream_len.item()) > 0
         if self.nfrag > 1:
             d = self.offsets[1:] - self.offsets[:-1]
             ok = ok and bool(torch.equal(d, self.comp_len[:-1].to(torch.int64)))

@@ -52,6 +52,9 @@ enum {
 enum { SM_MODE_REFERENCE = 0, SM_MODE_FAST = 1, SM_MODE_FAST_DENSE = 2 };
 
 #define SM_BLOCK_SIZE 65536u /* src/internal.jl:31 K_BLOCK_SIZE */
+/* d_out_len[b] >= SM_OUT_LEN_ERROR: block b failed (see sm_compress_batch_device).  The
+ * reference raises instead of returning a length (src/Snappy.jl:21). */
+#define SM_OUT_LEN_ERROR 0xfff00000u
 
 typedef struct sm_ctx sm_ctx;
 
@@ -99,9 +102,16 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t compressed_l
  * Block b: input d_in[d_in_off[b] .. +d_in_len[b]), d_in_len[b] <= 65536; each block becomes
  * an independent snappy stream (varint header + one compress_fragment!, i.e. exactly
  * compress(block) of src/Snappy.jl:20-36) written at d_out + d_out_off[b], which must have
- * room for sm_max_compressed_length(d_in_len[b]) bytes.  d_out_len[b] receives its size
- * (0xffffffff if the block was longer than 64 KiB).  stream: the hipStream_t to launch on
- * (NULL = the default stream, as everywhere in HIP); nothing is synchronised. */
+ * room for sm_max_compressed_length(d_in_len[b]) bytes.  d_out_len[b] receives its size, or
+ * an error mark >= SM_OUT_LEN_ERROR (no stream was written for that block):
+ *   0xffffffff            the block was longer than 64 KiB;
+ *   SM_OUT_LEN_ERROR | k  the device parse failed internally (k != 0: a bounded wait between
+ *                         the kernel's waves gave up; never expected -- report it as a device
+ *                         error, SM_ERR_DEVICE).
+ * Every mark is larger than any real size (<= sm_max_compressed_length(65536) = 76,490); the
+ * host-buffer entry points check the lengths and return SM_ERR_DEVICE / SM_ERR_ARGUMENT instead
+ * of a mark.  stream: the hipStream_t to launch on (NULL = the default stream, as everywhere in
+ * HIP); nothing is synchronised. */
 sm_status sm_compress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
                                    const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                    const uint64_t* d_out_off, uint32_t* d_out_len, int mode, void* stream);

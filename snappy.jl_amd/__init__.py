@@ -34,6 +34,8 @@ BLOCK_SIZE = 65536
 
 SM_OK = 0
 SM_BUFFER_TOO_SMALL = 2
+SM_ERR_DEVICE = 32
+SM_OUT_LEN_ERROR = 0xFFF00000  # d_out_len[b] >= this: block b failed (include/snappy_mi355x.h)
 MODES = {"reference": 0, "fast": 1, "dense": 2}
 
 # exported symbols of include/snappy_mi355x.h (checked by tests/test_abi.py)
@@ -73,71 +75,77 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise OSError("libsnappy_mi355x.so not built (run __graft_entry__.build())")
-        L = ctypes.CDLL(LIB_PATH)
-        vp, sz, i32, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_uint32
-        L.sm_status_message.restype = ctypes.c_char_p
-        L.sm_status_message.argtypes = [i32]
-        L.sm_max_compressed_length.restype = sz
-        L.sm_max_compressed_length.argtypes = [sz]
-        L.sm_uncompressed_length.restype = i32
-        L.sm_uncompressed_length.argtypes = [vp, sz, ctypes.POINTER(sz)]
-        L.sm_parse32.restype = i32
-        L.sm_parse32.argtypes = [vp, sz, sz, ctypes.POINTER(u32), ctypes.POINTER(sz)]
-        L.sm_encode32.restype = sz
-        L.sm_encode32.argtypes = [vp, u32]
-        L.sm_ctx_create.restype = vp
-        L.sm_ctx_create.argtypes = [ctypes.c_int]
-        L.sm_ctx_destroy.restype = None
-        L.sm_ctx_destroy.argtypes = [vp]
-        L.sm_ctx_stream.restype = vp
-        L.sm_ctx_stream.argtypes = [vp]
-        L.sm_compress.restype = i32
-        L.sm_compress.argtypes = [vp, vp, sz, vp, ctypes.POINTER(sz), ctypes.c_int]
-        L.sm_uncompress.restype = i32
-        L.sm_uncompress.argtypes = [vp, vp, sz, vp, ctypes.POINTER(sz)]
-        L.sm_compress_batch_device.restype = i32
-        L.sm_compress_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int, vp]
-        L.sm_uncompress_batch_device.restype = i32
-        L.sm_uncompress_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
-        L.sm_compress_batch.restype = i32
-        L.sm_compress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
-        L.sm_uncompress_batch.restype = i32
-        L.sm_uncompress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
-        L.sm_compress_batch_sharded.restype = i32
-        L.sm_compress_batch_sharded.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
-        L.sm_uncompress_batch_sharded.restype = i32
-        L.sm_uncompress_batch_sharded.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp, vp, vp, vp]
-        L.sm_find_match_length.restype = i32
-        L.sm_find_match_length.argtypes = [vp, sz, sz, sz, sz, ctypes.POINTER(sz)]
-        L.sm_ctx_last_path.restype = ctypes.c_int
-        L.sm_ctx_last_path.argtypes = [vp]
-        L.sm_version.restype = ctypes.c_char_p
-        L.sm_version.argtypes = []
-        L.sm_compress_fragments_device.restype = i32
-        L.sm_compress_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp]
-        L.sm_validate_batch_device.restype = i32
-        L.sm_validate_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp]
-        L.sm_uncompressed_length_batch_device.restype = i32
-        L.sm_uncompressed_length_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
-        L.sm_validate_compressed_buffer.restype = i32
-        L.sm_validate_compressed_buffer.argtypes = [vp, vp, sz]
-        L.sm_uncompress_fragments_device.restype = i32
-        L.sm_uncompress_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
-        # snappy-c.h shape (test/libsnappy.jl:5-30): (char*, size_t, char*, size_t*) -> int
-        L.sm_snappy_compress.restype = i32
-        L.sm_snappy_compress.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
-        L.sm_snappy_uncompress.restype = i32
-        L.sm_snappy_uncompress.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
-        L.sm_snappy_max_compressed_length.restype = sz
-        L.sm_snappy_max_compressed_length.argtypes = [sz]
-        L.sm_snappy_uncompressed_length.restype = i32
-        L.sm_snappy_uncompressed_length.argtypes = [vp, sz, ctypes.POINTER(sz)]
-        L.sm_snappy_validate_compressed_buffer.restype = i32
-        L.sm_snappy_validate_compressed_buffer.argtypes = [vp, sz]
-        L.sm_snappy_set_mode.restype = i32
-        L.sm_snappy_set_mode.argtypes = [ctypes.c_int]
-        _lib = L
+        _lib = load_library(LIB_PATH)
     return _lib
+
+
+def load_library(path):
+    """A build of the C ABI at `path` with its prototypes set (lib() uses the shipped one; the
+    GPU tests also load diagnostic variants built by the Makefile, e.g. the error-mark build)."""
+    L = ctypes.CDLL(path)
+    vp, sz, i32, u32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int32, ctypes.c_uint32
+    L.sm_status_message.restype = ctypes.c_char_p
+    L.sm_status_message.argtypes = [i32]
+    L.sm_max_compressed_length.restype = sz
+    L.sm_max_compressed_length.argtypes = [sz]
+    L.sm_uncompressed_length.restype = i32
+    L.sm_uncompressed_length.argtypes = [vp, sz, ctypes.POINTER(sz)]
+    L.sm_parse32.restype = i32
+    L.sm_parse32.argtypes = [vp, sz, sz, ctypes.POINTER(u32), ctypes.POINTER(sz)]
+    L.sm_encode32.restype = sz
+    L.sm_encode32.argtypes = [vp, u32]
+    L.sm_ctx_create.restype = vp
+    L.sm_ctx_create.argtypes = [ctypes.c_int]
+    L.sm_ctx_destroy.restype = None
+    L.sm_ctx_destroy.argtypes = [vp]
+    L.sm_ctx_stream.restype = vp
+    L.sm_ctx_stream.argtypes = [vp]
+    L.sm_compress.restype = i32
+    L.sm_compress.argtypes = [vp, vp, sz, vp, ctypes.POINTER(sz), ctypes.c_int]
+    L.sm_uncompress.restype = i32
+    L.sm_uncompress.argtypes = [vp, vp, sz, vp, ctypes.POINTER(sz)]
+    L.sm_compress_batch_device.restype = i32
+    L.sm_compress_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int, vp]
+    L.sm_uncompress_batch_device.restype = i32
+    L.sm_uncompress_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+    L.sm_compress_batch.restype = i32
+    L.sm_compress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
+    L.sm_uncompress_batch.restype = i32
+    L.sm_uncompress_batch.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+    L.sm_compress_batch_sharded.restype = i32
+    L.sm_compress_batch_sharded.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp, vp, ctypes.c_int]
+    L.sm_uncompress_batch_sharded.restype = i32
+    L.sm_uncompress_batch_sharded.argtypes = [vp, ctypes.c_int, vp, vp, vp, u32, vp, vp, vp, vp, vp]
+    L.sm_find_match_length.restype = i32
+    L.sm_find_match_length.argtypes = [vp, sz, sz, sz, sz, ctypes.POINTER(sz)]
+    L.sm_ctx_last_path.restype = ctypes.c_int
+    L.sm_ctx_last_path.argtypes = [vp]
+    L.sm_version.restype = ctypes.c_char_p
+    L.sm_version.argtypes = []
+    L.sm_compress_fragments_device.restype = i32
+    L.sm_compress_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, ctypes.c_uint64, ctypes.c_int, vp]
+    L.sm_validate_batch_device.restype = i32
+    L.sm_validate_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp]
+    L.sm_uncompressed_length_batch_device.restype = i32
+    L.sm_uncompressed_length_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
+    L.sm_validate_compressed_buffer.restype = i32
+    L.sm_validate_compressed_buffer.argtypes = [vp, vp, sz]
+    L.sm_uncompress_fragments_device.restype = i32
+    L.sm_uncompress_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
+    # snappy-c.h shape (test/libsnappy.jl:5-30): (char*, size_t, char*, size_t*) -> int
+    L.sm_snappy_compress.restype = i32
+    L.sm_snappy_compress.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
+    L.sm_snappy_uncompress.restype = i32
+    L.sm_snappy_uncompress.argtypes = [vp, sz, vp, ctypes.POINTER(sz)]
+    L.sm_snappy_max_compressed_length.restype = sz
+    L.sm_snappy_max_compressed_length.argtypes = [sz]
+    L.sm_snappy_uncompressed_length.restype = i32
+    L.sm_snappy_uncompressed_length.argtypes = [vp, sz, ctypes.POINTER(sz)]
+    L.sm_snappy_validate_compressed_buffer.restype = i32
+    L.sm_snappy_validate_compressed_buffer.argtypes = [vp, sz]
+    L.sm_snappy_set_mode.restype = i32
+    L.sm_snappy_set_mode.argtypes = [ctypes.c_int]
+    return L
 
 
 def status_message(code):

@@ -427,6 +427,16 @@ sm_status gather_to_host(sm_ctx* ctx, const uint8_t* d_src, const uint64_t* d_sr
   return SM_OK;
 }
 
+// The compressor's lengths as the host receives them: a length above the block's bound is an
+// error mark (SM_OUT_LEN_ERROR | k: a bounded wait inside the kernel gave up; 0xffffffff: a block
+// over 64 KiB, rejected before the launch here).  Checked before any length is summed, allocated
+// or gathered, so a mark never becomes a copy size.
+sm_status check_compressed_lengths(const uint32_t* out_len, const uint32_t* in_len, uint32_t nblk) {
+  for (uint32_t b = 0; b < nblk; ++b)
+    if (out_len[b] > sm::max_compressed_length(in_len[b])) return out_len[b] >= SM_OUT_LEN_ERROR ? SM_ERR_DEVICE : SM_ERR_ARGUMENT;
+  return SM_OK;
+}
+
 bool valid_ctxs(sm_ctx* const* ctxs, int nctx) {
   if (!ctxs || nctx <= 0) return false;
   for (int i = 0; i < nctx; ++i) {
@@ -648,6 +658,8 @@ sm_status sm_compress_batch(sm_ctx* ctx, const uint8_t* in, const uint64_t* in_o
   SM_CHECK(sm::launch_compress(a, mode, s));
   SM_CHECK(hipMemcpyAsync(out_len, d_out_len, 4 * (size_t)nblk, hipMemcpyDeviceToHost, s));
   SM_CHECK(hipStreamSynchronize(s));
+  const sm_status lst = check_compressed_lengths(out_len, in_len, nblk);
+  if (lst != SM_OK) return lst;
   // copy back only each block's bytes
   return gather_to_host(ctx, (const uint8_t*)ctx->out.p, d_out_off, d_out_len, out_len, nblk, out_off, out);
 }
@@ -837,6 +849,10 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   SM_CHECK(hipMemcpyAsync(out_len.data(), d_out_len, 4 * (size_t)nfrag, hipMemcpyDeviceToHost, s));
   SM_CHECK(hipStreamSynchronize(s));
   HT("compress: kernels + lengths")
+  {
+    const sm_status lst = check_compressed_lengths(out_len.data(), in_len.data(), nfrag);
+    if (lst != SM_OK) return lst;
+  }
   size_t total = 0;
   for (uint32_t i = 0; i < nfrag; ++i) {
     dst_off[i] = total;

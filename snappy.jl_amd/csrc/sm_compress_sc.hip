@@ -16,8 +16,10 @@
 //     parity g & 1 picks the slot a position is written to, and the returned dword gives both
 //     candidates at once -- the latest earlier position of the same hash in the own slot (exact:
 //     a wave's LDS instructions execute in order, and the conflicting lanes of one instruction in
-//     ascending lane order) and the latest one of the other parity.  Correctness never depends on
-//     that order (every candidate is verified); only the ratio does;
+//     ascending lane order -- observed on gfx950, not an ISA guarantee) and the latest one of the
+//     other parity.  Correctness never depends on that order: a candidate is used only when it is
+//     an earlier position (C checks c - 1 < q, the one compare a nonzero test costs) and its
+//     bytes match; only the ratio depends on it;
 //  C. checks both candidates' first 4 bytes and keeps the more recent one that matches, or the
 //     older one when the recent one is nearer than SC_FAR (256) bytes and the older matches too
 //     (fewer copies that read the decoder's own tag batch): per position its offset (u16, rows of
@@ -391,13 +393,16 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t sh = 16 * (g & 1);
     const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
     const uint32_t c1 = (SC_ABL & 8) ? 0u : max(ca, cb), c2 = (SC_ABL & 8) ? 0u : min(ca, cb);
-    // A nonzero candidate is always an earlier position: the table is cleared per block and
-    // filled in position order (the own slot by lower lanes of the same instruction or earlier
-    // groups, the other slot by earlier groups).  Positions without 4 bytes before the block end
-    // exchanged with the dummy word, and positions without 4 bytes before the super-chunk end may
-    // not start a copy: the walks' row masks leave both out (D), so no per-group check here.  The
-    // loads of a rejected candidate read the position itself.
-    const bool ok1 = c1 != 0, ok2 = c2 != 0;
+    // A candidate is valid when it is an earlier position: c - 1 < q (unsigned, so 0 = empty
+    // fails too).  The table is cleared per block and filled in position order, so a nonzero
+    // entry is an earlier position whenever the conflicting lanes of one ds_mskor_rtn are
+    // serviced in ascending lane order (observed on gfx950); the compare makes validity
+    // independent of that order, at the cost of the nonzero test it replaces.
+    // Positions without 4 bytes before the block end exchanged with the dummy word, and positions
+    // without 4 bytes before the super-chunk end may not start a copy: the walks' row masks leave
+    // both out (D), so no per-group check here.  The loads of a rejected candidate read the
+    // position itself.
+    const bool ok1 = c1 - 1u < q, ok2 = c2 - 1u < q;
     const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
     const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
     if constexpr (kDense) {

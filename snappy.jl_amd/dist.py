@@ -20,6 +20,7 @@ distributed logic with gloo, using the oracle as a stand-in for the GPU kernels.
 import numpy as np
 
 BLOCK = 65536
+SM_OUT_LEN_ERROR = 0xFFF00000  # include/snappy_mi355x.h: d_out_len error marks
 
 
 def shard_range(nitems, rank, world):
@@ -110,7 +111,12 @@ def stream_offsets_device(local_sizes, total_len, rank, world, group=None):
     exclusive scan behind the varint(total_len) header.  local_sizes: this rank's fragment
     sizes on the collective device.  Shard sizes are static (shard_range), so there is no host
     round trip: every rank pads to the largest shard.  Returns (global offsets of this rank's
-    fragments, the stream's total length as a 1-element tensor) on local_sizes' device."""
+    fragments, the stream's total length as a 1-element tensor) on local_sizes' device.
+
+    The all-gather runs whenever a process group is up, world 1 included (so the RCCL path is
+    the one measured at any world size).  A fragment whose size is a compressor error mark
+    (>= SM_OUT_LEN_ERROR = 0xfff00000 as u32, i.e. negative as torch int32) poisons the result
+    without a host round trip: the returned total is -1 on every rank."""
     import torch
     import torch.distributed as dist
     nfrag = (total_len + BLOCK - 1) // BLOCK
@@ -120,7 +126,7 @@ def stream_offsets_device(local_sizes, total_len, rank, world, group=None):
     hl = len(varint32(total_len))
     if nfrag == 0:  # an empty stream: the header alone
         return torch.zeros(0, dtype=torch.int64, device=dev), torch.full((1,), hl, dtype=torch.int64, device=dev)
-    if world == 1:
+    if world == 1 and not (dist.is_available() and dist.is_initialized()):
         sizes = local_sizes.to(torch.int64)
     else:
         buf = torch.zeros(m, dtype=torch.int64, device=dev)
@@ -128,7 +134,10 @@ def stream_offsets_device(local_sizes, total_len, rank, world, group=None):
         parts = [torch.empty_like(buf) for _ in range(world)]
         dist.all_gather(parts, buf, group=group)
         sizes = torch.cat([p[: hi - lo] for p, (lo, hi) in zip(parts, bounds)])
+    sizes = sizes & 0xFFFFFFFF  # (u32 sizes held in int32 tensors)
+    bad = (sizes >= SM_OUT_LEN_ERROR).any()
     incl = torch.cumsum(sizes, 0)
     starts = hl + incl - sizes
     lo, hi = bounds[rank]
-    return starts[lo:hi], incl[-1:] + hl
+    total = torch.where(bad, torch.full((1,), -1, dtype=torch.int64, device=dev), incl[-1:] + hl)
+    return starts[lo:hi], total

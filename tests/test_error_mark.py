@@ -1,0 +1,102 @@
+"""The fast compressor's internal-failure mark.
+
+k_compress_sc bounds every hand-off wait between its waves; a wait that gives up makes the
+block's d_out_len an error mark (SM_OUT_LEN_ERROR | k, include/snappy_mi355x.h), never a
+length.  The host entry points must turn a mark into SM_ERR_DEVICE -- not SM_BUFFER_TOO_SMALL,
+and never a gather of gigabytes.  The reference raises instead of returning data
+(src/Snappy.jl:21,50).
+
+The shipped library never times out, so these tests load the diagnostic build
+libsnappy_mi355x_spin0.so (the Makefile's `variants` target: -DSC_SPIN_BITS=0, every wait gives
+up after two polls) through the same prototypes as the product.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, read_testfile
+
+pytestmark = pytest.mark.gpu
+
+VARIANT = os.path.join(ROOT, "snappy.jl_amd", "libsnappy_mi355x_spin0.so")
+
+
+@pytest.fixture(scope="module")
+def spin0(sm, gpu_available):
+    if not os.path.exists(VARIANT):
+        pytest.fail("diagnostic build %s missing (make -C snappy.jl_amd/csrc variants)" % VARIANT)
+    L = sm.load_library(VARIANT)
+    ctx = L.sm_ctx_create(0)
+    assert ctx
+    yield L, ctx
+    L.sm_ctx_destroy(ctx)
+
+
+def _text_blocks(n):
+    raw = read_testfile("lcet10.txt") + read_testfile("plrabn12.txt")
+    return [raw[(7919 * i) % (len(raw) - 65536):][:65536] for i in range(n)]
+
+
+def test_batch_host_api_reports_device_error(sm, spin0):
+    L, ctx = spin0
+    blocks = _text_blocks(64)
+    buf, in_off, in_len = sm.pack_blocks(blocks)
+    out_off, caps = sm.slot_offsets(in_len)
+    out = np.zeros(int(out_off[-1] + caps[-1]), dtype=np.uint8)
+    out_len = np.zeros(len(blocks), dtype=np.uint32)
+    st = L.sm_compress_batch(ctx, buf.ctypes.data, in_off.ctypes.data, in_len.ctypes.data, len(blocks),
+                             out.ctypes.data, out_off.ctypes.data, out_len.ctypes.data, sm.MODES["fast"])
+    assert st == sm.SM_ERR_DEVICE, st
+    marks = out_len[out_len >= sm.SM_OUT_LEN_ERROR]
+    assert marks.size > 0 and np.all((marks & 0xFFFFF) != 0), out_len[:8]
+    # no mark became a gather: nothing was written into the caller's output
+    assert not out.any()
+
+
+def test_single_buffer_api_reports_device_error(sm, spin0):
+    L, ctx = spin0
+    raw = np.frombuffer(b"".join(_text_blocks(8)), dtype=np.uint8)
+    cap = sm.maxlength_compressed(raw.size)
+    out = np.zeros(cap, dtype=np.uint8)
+    ol = ctypes.c_size_t(cap)
+    st = L.sm_compress(ctx, raw.ctypes.data, raw.size, out.ctypes.data, ctypes.byref(ol), sm.MODES["fast"])
+    assert st == sm.SM_ERR_DEVICE, st  # (round 3: SM_BUFFER_TOO_SMALL, inviting a retry)
+
+
+def test_device_api_writes_marks(sm, spin0):
+    import torch
+    L, ctx = spin0
+    blocks = _text_blocks(32)
+    buf, in_off, in_len = sm.pack_blocks(blocks)
+    out_off, caps = sm.slot_offsets(in_len)
+    dev = torch.device("cuda", 0)
+    d_in = torch.from_numpy(buf.copy()).to(dev)
+    d_in_off = torch.from_numpy(in_off.astype(np.int64)).to(dev)
+    d_in_len = torch.from_numpy(in_len.astype(np.int32)).to(dev)
+    d_out = torch.zeros(int(out_off[-1] + caps[-1]), dtype=torch.uint8, device=dev)
+    d_out_off = torch.from_numpy(out_off.astype(np.int64)).to(dev)
+    d_out_len = torch.zeros(len(blocks), dtype=torch.int32, device=dev)
+    st = L.sm_compress_batch_device(ctx, d_in.data_ptr(), d_in_off.data_ptr(), d_in_len.data_ptr(), len(blocks),
+                                    d_out.data_ptr(), d_out_off.data_ptr(), d_out_len.data_ptr(), sm.MODES["fast"],
+                                    None)
+    assert st == 0
+    torch.cuda.synchronize()
+    lens = d_out_len.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    assert np.any(lens >= sm.SM_OUT_LEN_ERROR), lens[:8]
+    # every other length is a real one (a block whose waits all happened to succeed)
+    ok = lens < sm.SM_OUT_LEN_ERROR
+    assert np.all(lens[ok] <= sm.maxlength_compressed(65536))
+    # dist.stream_offsets_device poisons the stream total on a mark, without a host round trip
+    D = __import__("snappy_jl_amd.dist", fromlist=["stream_offsets_device"])
+    _, total = D.stream_offsets_device(d_out_len, 32 * 65536, 0, 1)
+    assert int(total.item()) == -1
+
+
+def test_shipped_library_has_no_marks(sm, gpu_available):
+    """The product on the same blocks: real lengths, SM_OK, streams that decode."""
+    blocks = _text_blocks(64)
+    outs = sm.compress_batch(blocks, mode="fast")
+    dec, st = sm.uncompress_batch(outs)
+    assert not st.any() and dec == blocks

@@ -35,10 +35,10 @@ def test_kernel_register_budgets(tmp_path):
             m = re.search(r"remark:\s+(VGPRs|VGPRs Spill|Occupancy \[waves/SIMD\]): (\d+)", line)
             if m and name:
                 usage[name][m.group(1)] = int(m.group(2))
-    fast = [k for k in usage if "k_compress_fast" in k]
-    assert len(fast) == 2, usage.keys()
-    for k in fast:
-        assert usage[k]["VGPRs"] < 128 and usage[k]["VGPRs Spill"] == 0, (k, usage[k])
+    # sm_compress_fast.hip holds only the incompressible screen (the round-2 parse is gone)
+    assert not [k for k in usage if "k_compress_fast" in k], usage.keys()
+    scr = [k for k in usage if "k_literal_screen" in k]
+    assert len(scr) == 1 and usage[scr[0]]["VGPRs Spill"] == 0, usage.get(scr[0] if scr else None)
     # the shipped fast compressor (sm_compress_sc.hip, fast and dense instances): 16-wave
     # workgroups, so at most 128 VGPRs, and at most 8 spilled dwords -- block-level values stored
     # once per block, outside the super-chunk loop (the lane index is laundered per super-chunk so
