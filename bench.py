@@ -49,7 +49,7 @@ BLOCK = 65536
 SLOT = 76496  # >= max_compressed_length(65536) = 76490, 16-B aligned
 HBM_PEAK_GBPS = 8000.0
 METRIC = "GB/s compressed+decompressed (batched blocks) at 1/2/4/8 GPUs; % HBM peak"  # BASELINE.json
-ROUND = "r03"
+ROUND = "r04"
 
 # test/runtests.jl:8-24, the round-trip corpus; config 5 tiles it
 ROUNDTRIP_FILES = ["alice29.txt", "asyoulik.txt", "html", "html_x_4", "kppkn.gtb", "lcet10.txt", "fireworks.jpeg",
@@ -636,6 +636,7 @@ def main():
         torch.cuda.empty_cache()
 
     if args.extras and rank == 0 and world == 1:
+        extras["single_call"] = single_call_table(sm)
         if big is None:
             big = large_corpus()
         extras["config5_host_stream"] = config5_host_stream(sm, big)
@@ -722,6 +723,54 @@ def extra_modes(sm, batch, in_bytes):
     out["reference_ok"] = batch.verify()
     batch.compress(sm, "fast")
     return out
+
+
+# test/benchmarks.jl:9-16 (the files) and README.md:37-45 (Julia 0.6 on a Mac, median of 10,000
+# calls; MB = 2^20 B; compress rates per input byte, uncompress rates per COMPRESSED byte,
+# test/benchmarks.jl:49,78)
+REFERENCE_SINGLE_CALL = {
+    "alice29.txt": ("txt", 243 * 2**20, 324 * 2**20),
+    "html": ("html", 672 * 2**20, 288 * 2**20),
+    "fireworks.jpeg": ("jpeg", 1.92 * 2**30, 6.73 * 2**30),
+    "paper-100k.pdf": ("pdf", 3.43 * 2**30, 4.24 * 2**30),
+    "urls.10K": ("urls", 357 * 2**20, 332 * 2**20),
+    "sample-tweet.json": ("json", 744 * 2**20, 420 * 2**20),
+}
+
+
+def single_call_table(sm, min_s=0.25, max_calls=2000):
+    """The drop-in single-buffer entry points (sm_compress / sm_uncompress: host buffers in and
+    out, PCIe and launch latency included) on the reference's own benchmark files, timed the way
+    test/benchmarks.jl times Snappy.jl: the median of repeated calls, compress rate per input
+    byte, uncompress rate per compressed byte (of the stream the same mode produced).  Each row
+    carries the reference's published Julia rate for the same file (README.md:37-45; other
+    hardware) and the decode path the library took."""
+    rows = {}
+    for fname, (tag, ref_c, ref_d) in REFERENCE_SINGLE_CALL.items():
+        data = open(os.path.join(TESTDATA, fname), "rb").read()
+        row = {"file": fname, "bytes": len(data)}
+        for mode in ("fast", "reference"):
+            comp = sm.compress(data, mode=mode)
+            assert sm.uncompress(comp) == data
+
+            def med(fn):
+                ts, t_end = [], time.perf_counter() + min_s
+                while len(ts) < 10 or (time.perf_counter() < t_end and len(ts) < max_calls):
+                    t0 = time.perf_counter()
+                    fn()
+                    ts.append(time.perf_counter() - t0)
+                return float(np.median(ts))
+            tc = med(lambda: sm.compress(data, mode=mode))
+            td = med(lambda: sm.uncompress(comp))
+            row[mode] = {"compressed_bytes": len(comp),
+                         "compress_us": round(tc * 1e6, 1), "compress_MBps": round(len(data) / tc / 2**20, 1),
+                         "uncompress_us": round(td * 1e6, 1), "uncompress_MBps": round(len(comp) / td / 2**20, 1),
+                         "uncompress_path": sm.last_uncompress_path()}
+        row["julia_published_MBps"] = {"compress": round(ref_c / 2**20, 1), "uncompress": round(ref_d / 2**20, 1)}
+        rows[tag] = row
+    return {"workload": "single calls from host buffers on test/benchmarks.jl's files; MB/s with MB = 2^20 B; "
+                        "uncompress per compressed byte; median over >= 10 calls",
+            "files": rows}
 
 
 if __name__ == "__main__":
