@@ -85,8 +85,12 @@ void* sm_ctx_stream(sm_ctx* ctx);
 /* diagnostic: how the ctx's last sm_uncompress decoded -- 0 in stream order (one wave),
  * 1 as parallel 64 KiB fragments (a large block-structured stream), 2 in parallel by origin
  * pointers (a large stream whose copies cross 64 KiB blocks), 3 a large stream's first error
- * found in parallel (per-tag checks over its tag path), -1 none yet */
+ * found in parallel (per-tag checks over its tag path), 4 a small stream (<= 1 MiB compressed)
+ * decoded in parallel by origin pointers entirely on the device (one synchronisation), -1 none yet */
 int sm_ctx_last_path(sm_ctx* ctx);
+/* diagnostic: enable (1, the default) or disable (0) path 4 for the ctx's sm_uncompress calls
+ * (the tests run the other paths on small streams with it off) */
+sm_status sm_ctx_set_small_decode(sm_ctx* ctx, int enable);
 
 /* ---- single buffer, host memory (the reference's exported API) -------------------- */
 /* replaces compress(::Vector{UInt8}), src/Snappy.jl:20-36 (and compress(::String), :38).

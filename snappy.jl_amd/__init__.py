@@ -43,7 +43,7 @@ ABI_SYMBOLS = (
     "sm_status_message", "sm_max_compressed_length", "sm_uncompressed_length", "sm_parse32",
     "sm_encode32", "sm_ctx_create", "sm_ctx_destroy", "sm_ctx_stream", "sm_compress", "sm_uncompress",
     "sm_compress_batch_device", "sm_uncompress_batch_device", "sm_compress_batch",
-    "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device", "sm_ctx_last_path",
+    "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device", "sm_ctx_last_path", "sm_ctx_set_small_decode",
     "sm_find_match_length", "sm_validate_batch_device", "sm_uncompressed_length_batch_device",
     "sm_validate_compressed_buffer", "sm_compress_batch_sharded", "sm_uncompress_batch_sharded",
     "sm_uncompress_fragments_device", "sm_snappy_compress", "sm_snappy_uncompress",
@@ -120,6 +120,8 @@ def load_library(path):
     L.sm_find_match_length.argtypes = [vp, sz, sz, sz, sz, ctypes.POINTER(sz)]
     L.sm_ctx_last_path.restype = ctypes.c_int
     L.sm_ctx_last_path.argtypes = [vp]
+    L.sm_ctx_set_small_decode.restype = ctypes.c_int
+    L.sm_ctx_set_small_decode.argtypes = [vp, ctypes.c_int]
     L.sm_version.restype = ctypes.c_char_p
     L.sm_version.argtypes = []
     L.sm_compress_fragments_device.restype = i32
@@ -257,8 +259,16 @@ def find_match_length(buf, i1, i2, limit):
 def last_uncompress_path(device=0):
     """How the last uncompress() on this device decoded: 0 in order, 1 parallel fragments
     (block-structured stream), 2 parallel by origin pointers (copies cross 64 KiB blocks), 3 a
-    large stream's first error found in parallel (its status returned, no output)."""
+    large stream's first error found in parallel (its status returned, no output), 4 a small
+    stream decoded by origin pointers entirely on the device."""
     return int(lib().sm_ctx_last_path(context(device)))
+
+
+def set_small_decode(enable, device=0):
+    """Diagnostic: path 4 (small streams on the device) on or off for uncompress() on this device."""
+    st = lib().sm_ctx_set_small_decode(context(device), 1 if enable else 0)
+    if st:
+        raise SnappyError(st)
 
 
 def uncompress(data, device=0):

@@ -81,6 +81,7 @@ struct sm_ctx {
   DevBuf in, out, out2, meta, idx, gat, org;  // org: origin pointers of the general parallel decode
   HostBuf stage;
   int last_path = -1;  // sm_ctx_last_path
+  bool small = true;   // sm_ctx_set_small_decode
   std::mutex mu;       // serialises the host-buffer entry points (they share the scratch above)
 };
 
@@ -351,6 +352,44 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
   return 2;
 }
 
+// A small stream entirely on the device (sm_decompress.hip, "a small stream"): index, chain,
+// origin pointers, resolve, gather, then one synchronisation with the output's download.
+// Returns 4 with the output in host_out, 0 to fall back (an error or anything unexpected: the
+// old paths find the reference's first error), -1 on a device error.
+#ifndef SM_SMALL_MIN
+#define SM_SMALL_MIN 4096
+#endif
+constexpr uint32_t kSmallMinOutput = SM_SMALL_MIN;  // smaller streams: the one-wave decode
+constexpr uint32_t kSmallMaxChunks = 1024;         // compressed bodies up to 1 MiB
+constexpr uint32_t kSmallMaxOutput = 64u << 20;    // 4 B of origin pointer per output byte
+
+int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8_t* host_out) {
+  using sm::kIdxEntries;
+  using sm::kSmallChunk;
+  const uint32_t nchunks = (n - ip0 + kSmallChunk - 1) / kSmallChunk;
+  uint32_t rounds = 1;  // kSmallHops^rounds >= size: every chain (at most size steps) resolves
+  for (uint64_t reach = sm::kSmallHops; reach < size; reach *= sm::kSmallHops) ++rounds;
+  const size_t path_off = align_up((size_t)nchunks * kIdxEntries * 8, 256);
+  const size_t ctl_off = align_up(path_off + (size_t)nchunks * sizeof(sm::OriginPath), 256);
+  const size_t ctl_n = 4 + rounds;
+  if (ctx->idx.ensure(ctl_off + ctl_n * 4) != hipSuccess) return 0;
+  if (ctx->org.ensure((size_t)size * 4) != hipSuccess) return 0;
+  hipStream_t s = ctx->stream;
+  uint8_t* ib = (uint8_t*)ctx->idx.p;
+  uint32_t* d_ctl = (uint32_t*)(ib + ctl_off);
+  if (hipMemsetAsync(d_ctl, 0, ctl_n * 4, s) != hipSuccess) return -1;
+  if (sm::launch_small_decode((const uint8_t*)ctx->in.p, n, ip0, size, nchunks, (uint32_t*)ib,
+                              (sm::OriginPath*)(ib + path_off), d_ctl, (uint32_t*)ctx->org.p, rounds,
+                              (uint8_t*)ctx->out.p, s) != hipSuccess)
+    return -1;
+  uint32_t ctl[4 + 32];
+  if (hipMemcpyAsync(ctl, d_ctl, ctl_n * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (hipMemcpyAsync(host_out, ctx->out.p, size, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  if (ctl[1] || ctl[2] || ctl[4 + rounds - 1]) return 0;  // (the last: never, by the round count)
+  return 4;
+}
+
 }  // namespace
 
 #define SM_CHECK(x)                 \
@@ -451,6 +490,13 @@ bool valid_ctxs(sm_ctx* const* ctxs, int nctx) {
 extern "C" {
 
 int sm_ctx_last_path(sm_ctx* ctx) { return ctx ? ctx->last_path : -1; }
+
+sm_status sm_ctx_set_small_decode(sm_ctx* ctx, int enable) {
+  if (!ctx) return SM_ERR_ARGUMENT;
+  std::lock_guard<std::mutex> lk(ctx->mu);
+  ctx->small = enable != 0;
+  return SM_OK;
+}
 
 const char* sm_status_message(sm_status st) {
   switch (st) {
@@ -902,6 +948,19 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   // and this library all write such streams); otherwise, or on any error, the in-order decode
   size_t hdr = 0;
   (void)sm_parse32((const uint8_t*)compressed, n, 0, &size, &hdr);
+  // (a body nearly as long as its output is mostly literals, which the in-order engine copies
+  // HBM to HBM at bandwidth: path 0 is faster there)
+  if (ctx->small && size >= kSmallMinOutput && size <= kSmallMaxOutput && n > hdr &&
+      (uint64_t)(n - hdr) * 8 <= (uint64_t)size * 7 &&
+      (n - hdr + sm::kSmallChunk - 1) / sm::kSmallChunk <= kSmallMaxChunks) {
+    const int r = small_uncompress(ctx, (uint32_t)n, (uint32_t)hdr, size, (uint8_t*)uncompressed);
+    if (r < 0) return SM_ERR_DEVICE;
+    if (r == 4) {
+      ctx->last_path = 4;
+      *uncompressed_length = size;
+      return SM_OK;
+    }
+  }
   if (size >= kParallelMinOutput && n - hdr >= 2 * sm::kIdxChunk) {
     bool copied = false;
     int32_t err = SM_OK;

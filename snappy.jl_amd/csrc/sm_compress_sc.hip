@@ -70,6 +70,20 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #ifndef SC_ABL
 #define SC_ABL 0
 #endif
+// Diagnostic builds only (-DSC_DUP=bits, tools/pmc_dup.sh): an LDS instruction group issued twice
+// (the copy idempotent or its result unused), so the PMC deltas against the plain build give the
+// group's own LDS-array and bank-conflict cycles: 1 the insert exchanges (B), 2 the candidate
+// loads (C), 4 the walks' position loads, 8 the walks' candidate loads, 16 the walks' offset
+// reads (D), 32 the staging ors (G), 64 the hash step's loads (A).
+#ifndef SC_DUP
+#define SC_DUP 0
+#endif
+// Reads served from the block in HBM/L1 (a raw buffer over [0, n): unaligned, no bank
+// conflicts, the vector-memory pipe instead of the LDS): 1 the candidate checks (C), 2 the walks'
+// position bytes, 4 the walks' candidate bytes (D).
+#ifndef SC_GC
+#define SC_GC 0
+#endif
 #ifndef SC_FAR  // fast mode: the older of two matching candidates when the recent one is nearer
 #define SC_FAR 256
 #endif
@@ -125,6 +139,18 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_wait(uint32_t* p, P
     if (SC_WSLEEP) __builtin_amdgcn_s_sleep(SC_WSLEEP);
   }
   return v;
+}
+
+// (SC_DUP) the five dwords at LDS byte address wa (dword-aligned) read again, the result dropped
+__device__ inline void sc_dup5(uint32_t wa) {
+  uint64_t x, y;
+  uint32_t z;
+  asm volatile("ds_read2_b32 %0, %3 offset1:1\nds_read2_b32 %1, %3 offset0:2 offset1:3\nds_read_b32 %2, %3 offset:16\n"
+               "s_waitcnt lgkmcnt(0)" : "=v"(x), "=v"(y), "=v"(z) : "v"(wa) : "memory");
+}
+__device__ inline void sc_dup2(uint32_t wa) {
+  uint64_t x;
+  asm volatile("ds_read2_b32 %0, %1 offset1:1\ns_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(wa) : "memory");
 }
 
 __device__ inline uint32_t sc_ld32(const uint8_t* blk, uint32_t a) { return *reinterpret_cast<const uint32_t*>(blk + a); }
@@ -204,6 +230,10 @@ __device__ inline void sc_lds_or(uint32_t a, uint4 v) {
   asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4\nds_or_b32 %0, %3 offset:8\nds_or_b32 %0, %4 offset:12\n"
                "ds_or_b32 %0, %5 offset:16"
                : : "v"(wa), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4) : "memory");
+  if (SC_DUP & 32)
+    asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4\nds_or_b32 %0, %3 offset:8\nds_or_b32 %0, %4 offset:12\n"
+                 "ds_or_b32 %0, %5 offset:16"
+                 : : "v"(wa), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4) : "memory");
 }
 
 // ors the (up to 3) bytes of cv into the zeroed LDS byte array at byte address a
@@ -211,6 +241,7 @@ __device__ inline void sc_lds_or3(uint32_t a, uint32_t cv) {
   const uint32_t wa = (a - 1u) & ~3u, t = (0u - a) & 3u;  // (as sc_lds_or)
   const uint32_t lo = __builtin_amdgcn_alignbyte(cv, 0u, t), hi = __builtin_amdgcn_alignbyte(0u, cv, t);
   asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
+  if (SC_DUP & 32) asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
 }
 
 // v shifted up by t (0..3) bytes with the t-byte value tag below it
@@ -306,7 +337,8 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_next_block(const Co
 // One super-chunk, by one wave (sections A-G2 above).
 template <int kDense>
 __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, const uint32_t k, const uint32_t n,
-                                                                   const uint32_t wave, const uint32_t lane_in) {
+                                                                   const uint32_t wave, const uint32_t lane_in,
+                                                                   const __amdgpu_buffer_rsrc_t gb) {
   // (the lane index laundered per super-chunk: otherwise the compiler hoists dozens of lane-derived
   // addresses out of the super-chunk loop, and the registers they hold serialise section C)
   uint32_t lane = lane_in;
@@ -325,6 +357,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
     const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, qa + 64 * g + 4), sc_ld32(S.blk, qa + 64 * g), qb);
+    if (SC_DUP & 64) sc_dup2(lds_addr(S.blk + qa + 64 * g));
     wq[g] = w;
     ha[g] = Tbase + 4 * ((w * kHashMul) >> (32 - kScTabBits));
     hvv[g] = (g & 1) ? hv1 + ((64u * g) << 16) : hv0 + 64u * g;
@@ -367,6 +400,13 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       "ds_mskor_rtn_b32 %13, %29, %33, %47\n"
       "ds_mskor_rtn_b32 %14, %30, %32, %48\n"
       "ds_mskor_rtn_b32 %15, %31, %33, %49\n"
+#if SC_DUP & 1
+      "s_waitcnt lgkmcnt(0)\n"
+      "ds_mskor_b32 %16, %32, %34\nds_mskor_b32 %17, %33, %35\nds_mskor_b32 %18, %32, %36\nds_mskor_b32 %19, %33, %37\n"
+      "ds_mskor_b32 %20, %32, %38\nds_mskor_b32 %21, %33, %39\nds_mskor_b32 %22, %32, %40\nds_mskor_b32 %23, %33, %41\n"
+      "ds_mskor_b32 %24, %32, %42\nds_mskor_b32 %25, %33, %43\nds_mskor_b32 %26, %32, %44\nds_mskor_b32 %27, %33, %45\n"
+      "ds_mskor_b32 %28, %32, %46\nds_mskor_b32 %29, %33, %47\nds_mskor_b32 %30, %32, %48\nds_mskor_b32 %31, %33, %49\n"
+#endif
       "ds_write_b32 %50, %51\n"
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
@@ -421,7 +461,18 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       Wl.L[16 * r4 + 4 * ((i >> 2) ^ ((g >> 1) & 3)) + (i & 3)] = (uint8_t)enc;
       mbs[g] = ballot(l >= 4);
     } else {
-      uint32_t v1 = lds_ld32(S.blk, p1), v2 = lds_ld32(S.blk, p2);
+      uint32_t v1, v2;
+      if (SC_GC & 1) {
+        v1 = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)p1, 0, 0);
+        v2 = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)p2, 0, 0);
+      } else {
+        v1 = lds_ld32(S.blk, p1);
+        v2 = lds_ld32(S.blk, p2);
+      }
+      if (SC_DUP & 2) {
+        sc_dup2(lds_addr(S.blk + (p1 & ~3u)));
+        sc_dup2(lds_addr(S.blk + (p2 & ~3u)));
+      }
       const uint32_t w = wq[g];
       asm("" : "+v"(v1), "+v"(v2));  // (keeps the loads unconditional)
       const bool m1 = ok1 && v1 == w, m2 = ok2 && v2 == w;
@@ -484,9 +535,29 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
             enc = Lrow[i ^ lsw4];  // (computed in C)
           } else {
             const uint32_t q = c0 + i, off = offAt(i);
-            const uint4 X = sc_ld128(S.blk, q);
+            uint4 X;
+            if (SC_GC & 2) {
+              const auto v = __builtin_amdgcn_raw_buffer_load_b128(gb, (int)q, 0, 0);
+              X = make_uint4(v[0], v[1], v[2], v[3]);
+            } else {
+              X = sc_ld128(S.blk, q);
+            }
             const uint32_t p = q - off;
-            const uint32_t l = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p & ~3u)), p & 3u);
+            if (SC_DUP & 4) sc_dup5(lds_addr(S.blk + (q & ~3u)));
+            if (SC_DUP & 8) sc_dup5(lds_addr(S.blk + (p & ~3u)));
+            if (SC_DUP & 16) {
+              uint32_t x;
+              asm volatile("ds_read_u16 %0, %1\ns_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(lds_addr(&Orow[i ^ osw2])) : "memory");
+            }
+            uint32_t l;
+            if (SC_GC & 4) {
+              const auto v = __builtin_amdgcn_raw_buffer_load_b128(gb, (int)p, 0, 0);
+              const uint32_t b0 = sc_ffbl(X.x ^ v[0]), b1 = sc_ffbl(X.y ^ v[1]) | 32u;
+              const uint32_t b2 = sc_ffbl(X.z ^ v[2]) | 64u, b3 = sc_ffbl(X.w ^ v[3]) | 96u;
+              l = min(min(b0, b1), min(min(b2, b3), 128u)) >> 3;
+            } else {
+              l = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p & ~3u)), p & 3u);
+            }
             const uint32_t avail = sce - q;
             enc = (l == 16 && avail > 16) ? kScExt : min(l, avail);
             Lrow[i ^ lsw4] = (uint8_t)enc;
@@ -836,6 +907,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
     __syncthreads();
 
     const uint32_t nsc = (n + kScS - 1) / kScS;
+    const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, (int)n, 0x00020000);
     if (wave == kScWorkers) {
       __builtin_amdgcn_s_setprio(SC_WPRIO);  // (the writer's chain gates the slots)
       sc_writer(S, a, b, n, dst, hv, nsc, lane);
@@ -847,7 +919,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
         // every lane adds 1 (one ds_add of 64 after the atomic optimizer); lane 0 sees a multiple of 64
         const uint32_t k = uniform(__hip_atomic_fetch_add(&S.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 6;
         if (k >= nsc) break;
-        sc_superchunk<kDense>(S, k, n, wave, lane);
+        sc_superchunk<kDense>(S, k, n, wave, lane, gb);
       }
     }
     SC_FETCH(bn)  // the next block's bytes, in flight behind the other waves' last super-chunks

@@ -717,18 +717,19 @@ __device__ inline uint32_t window_tags(const uint8_t* buf, uint32_t rel0, uint32
   return ntok;
 }
 
+template <uint32_t kC>  // compressed bytes per chunk (kIdxChunk; path 4: kSmallChunk)
 __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
                                                      uint2* rec) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kIdxChunk + kIdxPad];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kC + kIdxPad];
   __shared__ __attribute__((aligned(16))) uint16_t jt[6 * 256];  // walk tables, then the entry walk's 3 KiB
-  __shared__ uint32_t bm[kIdxChunk / 32];  // positions on lane 0's path
-  __shared__ uint32_t cum[kIdxChunk];      // output before each such position
+  __shared__ uint32_t bm[kC / 32];  // positions on lane 0's path
+  __shared__ uint32_t cum[kC];      // output before each such position
   const uint32_t c = blockIdx.x, lane = lane_id();
-  const uint32_t s = ip0 + c * kIdxChunk;
-  stage_bytes(buf, in, N, s, kIdxChunk + kIdxPad, lane);
-  for (uint32_t k = lane; k < kIdxChunk / 32; k += kWave) bm[k] = 0;
+  const uint32_t s = ip0 + c * kC;
+  stage_bytes(buf, in, N, s, kC + kIdxPad, lane);
+  for (uint32_t k = lane; k < kC / 32; k += kWave) bm[k] = 0;
   __syncthreads();
-  const uint64_t lim = min((uint64_t)s + kIdxChunk, (uint64_t)N - 1);  // tags start below N-1 (:416)
+  const uint64_t lim = min((uint64_t)s + kC, (uint64_t)N - 1);  // tags start below N-1 (:416)
   // lane 0's path: the tag walk from the chunk's first byte, a 256-byte window at a time
   uint64_t p = s, acc = 0, size, outb;
   while (p < lim) {
@@ -1002,17 +1003,18 @@ __device__ inline uint64_t load8z(const uint8_t* __restrict__ in, uint32_t N, ui
   return (uint64_t)load_word(in, N, p) | ((uint64_t)load_word(in, N, p + 4) << 32);
 }
 
-// kFill = false (k_path_check): the same walk without P, recording the reference's exact status
-// of the element's first failing tag (src/internal.jl:499, :505, :518) -- a stream's first error
-// is then the first failing element in path order, found in parallel instead of by the in-order
-// decode.  kErrCross marks an element whose tags do not tile it (the caller falls back).
+// One path element's tags by one wave (window walks, internal.jl:411-466), with the reference's
+// checks; kFill: the origin pointer of every output byte into P.  Returns the element's status.
+// stg (optional): the stream bytes [sb, sb + sl) staged in LDS (stage_bytes), read instead of HBM
 template <bool kFill>
-__global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
-                                                    const OriginPath* path, uint32_t* __restrict__ P,
-                                                    int32_t* status) {
-  __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
-  const uint32_t lane = lane_id();
-  const OriginPath pe = path[blockIdx.x];
+__device__ __attribute__((always_inline)) inline int32_t origin_walk(const uint8_t* __restrict__ in, uint32_t N,
+                                                                   uint32_t size, const OriginPath pe,
+                                                                   uint32_t* __restrict__ P, uint16_t* jt,
+                                                                   uint32_t lane, const uint8_t* stg = nullptr,
+                                                                   uint32_t sb = 0, uint32_t sl = 0) {
+  auto load8z = [&](const uint8_t* __restrict__ in_, uint32_t N_, uint32_t p) -> uint64_t {
+    return (stg && p >= sb && p - sb + 8 <= sl) ? lds_ld64(stg, p - sb) : sm::load8z(in_, N_, p);
+  };
   uint32_t ip = pe.y, op = pe.O;
   int32_t st = kOk;
   const uint32_t end = min(pe.ex, N - 1);  // a tag on the last byte is never parsed (internal.jl:416)
@@ -1064,19 +1066,169 @@ __global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ 
       st = kFill ? kErrInvalid : (int32_t)readlane((uint32_t)code, ctz64(bm));
       break;
     }
-    // every output byte of the window's tags: tag t's bytes by the whole wave
-    for (uint32_t t = 0; t < ntok; ++t) {
-      const uint32_t o = readlane(opt, t), L = readlane(olen, t);
-      const uint32_t v0 = readlane(iscopy ? 0u - offset : (0x80000000u | lsrc) - o, t);  // P[o+i] = o + i + v0
-      if (kFill)
-        for (uint32_t i = lane; i < L; i += kWave) P[o + i] = o + i + v0;
+    // every output byte of the window's tags: tag t's bytes by the whole wave.  A copy's byte i
+    // points at o - f + (i mod f): for i >= f its source lies inside the same copy, whose byte
+    // i - f is byte (i mod f) of the period (incremental_copy!, internal.jl:491-509) -- so a run
+    // (offset 1, 2, ...) adds one chain step, not one per period.
+    if (kFill) {  // each lane its own tag's pointers, four a store (P[o + i] = base + i')
+      const uint32_t base = iscopy ? opt - offset : 0x80000000u | lsrc;
+      const uint32_t f = iscopy && offset < olen ? offset : 0xffffffffu;  // a copy overlapping itself
+      uint32_t* const dst = P + opt;
+      uint32_t i = 0, r = 0;  // r = i mod f
+      auto nx = [&]() { r = r + 1 == f ? 0u : r + 1; };
+      while (ballot(i + 4 <= olen)) {
+        if (i + 4 <= olen) {
+          uint4 v;
+          v.x = base + r;
+          nx();
+          v.y = base + r;
+          nx();
+          v.z = base + r;
+          nx();
+          v.w = base + r;
+          nx();
+          *reinterpret_cast<uint4 __attribute__((aligned(4)))*>(dst + i) = v;
+          i += 4;
+        }
+      }
+      while (ballot(i < olen)) {
+        if (i < olen) {
+          dst[i] = base + r;
+          nx();
+          ++i;
+        }
+      }
     }
     op += readlane(incl, ntok - 1);
     ip += readlane(cpos + csz, ntok - 1);
   }
   if (st == kOk && ip != pe.ex && !(ip >= end && pe.ex >= end)) st = kFill ? kErrInvalid : kErrCross;  // tags tile the path
   if (st == kOk && op != pe.O + pe.out) st = kFill ? kErrInvalid : kErrCross;
-  if (lane == 0) status[blockIdx.x] = st;
+  return st;
+}
+
+// kFill = false (k_path_check): the same walk without P, recording the reference's exact status
+// of the element's first failing tag (src/internal.jl:499, :505, :518) -- a stream's first error
+// is then the first failing element in path order, found in parallel instead of by the in-order
+// decode.  kErrCross marks an element whose tags do not tile it (the caller falls back).
+template <bool kFill>
+__global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
+                                                    const OriginPath* path, uint32_t* __restrict__ P,
+                                                    int32_t* status) {
+  __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
+  const int32_t st = origin_walk<kFill>(in, N, size, path[blockIdx.x], P, jt, lane_id());
+  if (lane_id() == 0) status[blockIdx.x] = st;
+}
+
+// ---- a small stream, all on the device (sm_uncompress): the index records chained by one wave
+// instead of the host, the origin pointers filled per path element, resolved in a fixed number of
+// launches and gathered -- one synchronisation for the whole call.  Any stream (no block
+// structure assumed); anything unexpected (an error, no progress, a length mismatch) is reported
+// in ctl[1] and the caller decodes the old way, which also finds the first error.
+constexpr uint32_t kChainLds = 256;  // chunks whose records the chain reads from LDS (128 KiB)
+constexpr uint32_t kFillStage = kSmallChunk + kIdxPad + 256;  // an element's tags and a window past them
+
+// Host tag walk (sm_api.hip host_walk) by one wave, uniform: where the tags from p leave [p, lim)
+// and their output.  For chunk entries deeper than the index covers.
+__device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint64_t p, uint64_t lim, uint64_t& exit_pos,
+                                uint64_t& produced) {
+  uint64_t o = 0;
+  while (p < lim) {
+    const uint64_t hv = load8z(in, N, (uint32_t)p);
+    const uint32_t c = uniform((uint32_t)hv & 0xff);
+    const uint32_t entry = char_entry(c);
+    const uint32_t taglen = entry >> 11;
+    const uint32_t tr = uniform((uint32_t)(hv >> 8));
+    const uint32_t trailer = taglen >= 4 ? tr : (tr & ((1u << (8 * taglen)) - 1u));
+    if (c & 3) {
+      p += 1 + taglen;
+      o += entry & 0xff;
+    } else {
+      const uint32_t lit = (entry & 0xff) + trailer;  // u32 wrap, as the reference
+      p += 1ull + taglen + lit;
+      o += lit;
+    }
+  }
+  exit_pos = p;
+  produced = o;
+}
+
+// ctl[0] = path elements, ctl[1] = 0 (the path covers exactly `size` bytes of output) or 1 (fall back)
+__global__ __launch_bounds__(64) void k_stream_chain(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
+                                                     uint32_t size, uint32_t nchunks, const uint2* __restrict__ rec,
+                                                     OriginPath* path, uint32_t* ctl) {
+  __shared__ uint2 srec[kChainLds * kIdxEntries];
+  const uint32_t lane = lane_id();
+  const bool inlds = nchunks <= kChainLds;
+  if (inlds)
+    for (uint32_t k = lane; k < nchunks * kIdxEntries; k += kWave) srec[k] = rec[k];
+  __syncthreads();
+  uint64_t y = ip0, O = 0;
+  uint32_t np = 0, bad = 0;
+  while (y < (uint64_t)N - 1) {  // internal.jl:416
+    const uint32_t c = (uint32_t)((y - ip0) / kSmallChunk);
+    const uint64_t base = ip0 + (uint64_t)c * kSmallChunk, l = y - base;
+    uint64_t ex, ot;
+    if (l < kIdxEntries) {
+      const uint2 r = inlds ? srec[c * kIdxEntries + l] : rec[c * kIdxEntries + l];
+      ex = uniform(r.x);
+      ot = uniform(r.y);
+    } else {
+      dev_walk(in, N, y, min(base + kSmallChunk, (uint64_t)N - 1), ex, ot);
+    }
+    if (np >= nchunks || ex <= y) {  // (never for a well-formed index: every element leaves its chunk)
+      bad = 1;
+      break;
+    }
+    if (lane == 0) {
+      const uint64_t Oc = min(O, (uint64_t)0xffffffffu);
+      path[np] = {(uint32_t)y, (uint32_t)min(ex, (uint64_t)0xffffffffu), (uint32_t)Oc,
+                  (uint32_t)min(ot, 0xffffffffull - Oc)};
+    }
+    ++np;
+    O += ot;
+    y = ex;
+    if (O > size) break;
+  }
+  if (O != size) bad = 1;
+  if (lane == 0) {
+    ctl[0] = np;
+    ctl[1] = bad;
+  }
+}
+
+// k_origin_fill for the device chain's path: elements past ctl[0] exit; a failing element sets ctl[2]
+__global__ __launch_bounds__(64) void k_origin_fill_dev(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
+                                                        const OriginPath* path, uint32_t* __restrict__ P,
+                                                        uint32_t* ctl) {
+  __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kFillStage + 16];
+  if (blockIdx.x >= uniform(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ||
+      uniform(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+    return;
+  const OriginPath pe = path[blockIdx.x];
+  stage_bytes(buf, in, N, pe.y, kFillStage, lane_id());  // (zero past N, as load8z)
+  __syncthreads();
+  const int32_t st = origin_walk<true>(in, N, size, pe, P, jt, lane_id(), buf, pe.y, kFillStage);
+  if (st != kOk && lane_id() == 0) atomicOr(&ctl[2], 1u);
+}
+
+// Pointer jumping with up to kHops chain steps per pointer per launch: after launch r every
+// unresolved pointer has moved >= kHops^(r+1) steps.  Launch r > 0 returns at once when launch
+// r - 1 left nothing pending (pend[r] counts waves with unresolved pointers after launch r).
+constexpr uint32_t kHops = kSmallHops;
+__global__ __launch_bounds__(256) void k_origin_resolve_hops(uint32_t* P, uint32_t size, uint32_t* pend, uint32_t r) {
+  if (r > 0 && __hip_atomic_load(&pend[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  uint32_t left = 0;
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < size; x += gridDim.x * blockDim.x) {
+    uint32_t v = P[x];
+    if (v >> 31) continue;
+#pragma unroll 1
+    for (uint32_t h = 0; h < kHops && !(v >> 31); ++h) v = P[v];  // v < x: an earlier byte of the chain
+    P[x] = v;
+    left += !(v >> 31);
+  }
+  if (__builtin_amdgcn_ballot_w64(left != 0) && lane_id() == 0) atomicAdd(&pend[r], 1u);
 }
 
 __global__ __launch_bounds__(256) void k_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending) {
@@ -1120,6 +1272,20 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
   return hipGetLastError();
 }
 
+hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
+                               uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
+                               uint8_t* out, hipStream_t s) {
+  if (nchunks == 0 || size == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_stream_index<kSmallChunk>, dim3(nchunks), dim3(64), 0, s, in, N, ip0, reinterpret_cast<uint2*>(rec));
+  hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(64), 0, s, in, N, ip0, size, nchunks,
+                     reinterpret_cast<const uint2*>(rec), path, ctl);
+  hipLaunchKernelGGL(k_origin_fill_dev, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
+  for (uint32_t r = 0; r < rounds; ++r)
+    hipLaunchKernelGGL(k_origin_resolve_hops, dim3(origin_grid(size)), dim3(256), 0, s, P, size, ctl + 4, r);
+  hipLaunchKernelGGL(k_origin_gather, dim3(origin_grid(size)), dim3(256), 0, s, in, P, size, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s) {
   if (size == 0) return hipSuccess;
   hipLaunchKernelGGL(k_origin_gather, dim3(origin_grid(size)), dim3(256), 0, s, in, P, size, out);
@@ -1129,7 +1295,7 @@ hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t s
 hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec,
                                hipStream_t s) {
   if (nchunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_stream_index, dim3(nchunks), dim3(64), 0, s, in, N, ip0, reinterpret_cast<uint2*>(rec));
+  hipLaunchKernelGGL(k_stream_index<kIdxChunk>, dim3(nchunks), dim3(64), 0, s, in, N, ip0, reinterpret_cast<uint2*>(rec));
   return hipGetLastError();
 }
 

@@ -44,6 +44,8 @@ hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 // compressed body, then one wave per 64 KiB output fragment (see sm_decompress.hip).
 constexpr uint32_t kIdxChunk = 4096;  // compressed bytes per index chunk
 constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
+constexpr uint32_t kSmallChunk = 1024;  // path 4 (a small stream on the device): bytes per index chunk
+constexpr uint32_t kSmallHops = 32;     // path 4: chain steps per pointer per resolve launch
 constexpr uint32_t kIdxPad = 288;     // staged bytes past a chunk: +16 entry slack, a 256-byte walk window + 16
 struct StreamFrag {
   uint32_t y;    // a true tag start at or before the fragment's first tag (chunk entry)
@@ -73,6 +75,14 @@ hipError_t launch_origin_fill(const uint8_t* in, uint32_t N, uint32_t size, cons
 hipError_t launch_path_check(const uint8_t* in, uint32_t N, uint32_t size, const OriginPath* path, uint32_t npath,
                              int32_t* status, hipStream_t s);
 hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, hipStream_t s);
+// A small stream entirely on the device (index, chain, fill, `rounds` resolve launches, gather; no
+// host synchronisation).  rec: nchunks * kIdxEntries u32 pairs; path: nchunks elements; ctl: 4 +
+// rounds zeroed u32 -- ctl[0] path elements, ctl[1] != 0: the chain found no exact path (fall
+// back), ctl[2] != 0: an element failed its checks (fall back), ctl[4 + r] != 0: pointers still
+// unresolved after round r.  P: size u32.
+hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
+                               uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
+                               uint8_t* out, hipStream_t s);
 hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)
 hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,

@@ -361,19 +361,39 @@ def _big_corpus(n):
     return (raw * (n // len(raw) + 1))[:n]
 
 
+def small_path(sm, comp):
+    """Whether sm_uncompress takes path 4 (small stream on the device, sm_api.hip
+    small_uncompress) for this stream: 4 KiB..64 MiB of output from a body of <= 1024 index
+    chunks of 1 KiB (1 MiB) and at most 7/8 of the output (else mostly literals: path 0)."""
+    size, hdr = sm.parse32(comp, 0)
+    body = len(comp) - hdr
+    return (4096 <= size <= (64 << 20) and body > 0 and (body + 1023) // 1024 <= 1024
+            and body * 8 <= size * 7)
+
+
 def test_uncompress_large_stream_parallel(sm, oracle, libsnappy, gpu_available):
     """Block-structured streams (Snappy.jl = oracle, libsnappy, this library's fast mode) of
-    more than 4 fragments decode through the parallel fragment path, bit-exactly."""
+    more than 4 fragments decode through the parallel fragment path, bit-exactly -- or, with a
+    body of at most 1 MiB, through path 4; with path 4 off, all through the fragment path."""
     raw = _big_corpus(1_500_000)
     rng = np.random.default_rng(9)
     noise = rng.integers(0, 256, 1_000_000, dtype=np.uint8).tobytes()
     mixed = b"".join(raw[i:i + 50_000] + noise[i:i + 30_000] for i in range(0, 900_000, 80_000))
     # every 64 KiB block starting with a long literal (> 200 B: the batch path's big literals)
     blocky = b"".join(noise[i * 1000:i * 1000 + 700] + raw[i * 65536:i * 65536 + 64836] for i in range(8))
-    for data in (raw, noise, mixed, blocky):
-        for comp in (oracle.compress(data), libsnappy.compress(data), sm.compress(data, mode="fast")):
-            assert sm.uncompress(comp) == data
-            assert sm.last_uncompress_path() == 1
+    seen = set()
+    try:
+        for small in (True, False):
+            sm.set_small_decode(small)
+            for data in (raw, noise, mixed, blocky):
+                for comp in (oracle.compress(data), libsnappy.compress(data), sm.compress(data, mode="fast")):
+                    assert sm.uncompress(comp) == data
+                    want = 4 if small and small_path(sm, comp) else 1
+                    assert sm.last_uncompress_path() == want
+                    seen.add(want)
+    finally:
+        sm.set_small_decode(True)
+    assert seen == {1, 4}
 
 
 def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
@@ -386,10 +406,15 @@ def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
     s1, e1 = build(random_ops(rng, 400_000))                        # offsets up to 65535
     s2, e2 = build([("lit", rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes())] +
                    [("copy", 1000, 64)] * 5000)                      # literal across 65536
-    for s, e in ((s1, e1), (s2, e2)):
-        assert oracle.uncompress(s) == e
-        assert sm.uncompress(s) == e
-        assert sm.last_uncompress_path() == 2
+    try:
+        for small in (True, False):
+            sm.set_small_decode(small)
+            for s, e in ((s1, e1), (s2, e2)):
+                assert oracle.uncompress(s) == e
+                assert sm.uncompress(s) == e
+                assert sm.last_uncompress_path() == (4 if small and small_path(sm, s) else 2)
+    finally:
+        sm.set_small_decode(True)
     good = oracle.compress(_big_corpus(600_000))
     paths = []
     for i in range(40):
@@ -561,11 +586,70 @@ def test_uncompress_origin_path_cases(sm, oracle, gpu_available):
         size += ln
     cases.append(build(ops))
     cases.append(build(random_ops(rng, 1_500_000, max_off=65535, near=60_000)))
+    try:
+        for small in (False, True):  # path 2, then path 4 (the same origin pointers, device-chained)
+            sm.set_small_decode(small)
+            for s, e in cases:
+                assert oracle.uncompress(s) == e
+                assert sm.uncompress(s) == e
+                assert sm.last_uncompress_path() == (4 if small and small_path(sm, s) else 2)
+                assert sm.validate(s) == 0
+    finally:
+        sm.set_small_decode(True)
+    assert sum(small_path(sm, s) for s, _ in cases) >= 3
+
+
+def test_uncompress_small_streams_device_path(sm, oracle, libsnappy, gpu_available):
+    """Path 4 (sm_api.hip small_uncompress; sm_decompress.hip k_stream_chain, k_origin_fill_dev,
+    k_origin_resolve_hops): every corpus file in every compress mode and from libsnappy, streams
+    at the path's size limits (4 KiB of output, one index chunk, 256 chunks), deep copy chains,
+    and mutated streams -- output and status equal the oracle's (test/runtests.jl:8-24 round
+    trips; internal.jl:411-466 errors, first in stream order)."""
+    from streams import build, random_ops
+    rng = np.random.default_rng(404)
+    cases = []
+    for f in ROUNDTRIP_FILES + ["sample-tweet.json"]:
+        raw = read_testfile(f)
+        cases += [(oracle.compress(raw), raw), (libsnappy.compress(raw), raw),
+                  (sm.compress(raw, mode="fast"), raw), (sm.compress(raw, mode="dense"), raw)]
+    text = _big_corpus(3_000_000)
+    for n in (4095, 4096, 4097, 5000, 65535, 65536, 65537, 200_000):
+        cases.append((oracle.compress(text[:n]), text[:n]))
+    # bodies of exactly 1, 4 and 1024 index chunks of 1 KiB and one byte more
+    for body in (1024, 1025, 4096, 4097, 1024 * 1024, 1024 * 1024 + 1):
+        ops, left = [("lit", rng.integers(0, 256, 60, dtype=np.uint8).tobytes())], body - 61
+        while left > 61:                      # copy-2 tags: 3 bytes for 60 bytes of output
+            ops.append(("copy", 60, 60))
+            left -= 3
+        ops.append(("lit", rng.integers(0, 256, left - 1, dtype=np.uint8).tobytes()))
+        st, ex = build(ops)
+        assert len(st) - len(sm.encode32(len(ex))) == body
+        cases.append((st, ex))
+    cases.append(build([("lit", b"ab")] + [("copy", 2, 64)] * 4000))             # one period-2 run
+    cases.append(build([("lit", b"q")] + [("copy", 1, 1)] * 20_000))             # 1-byte copies
+    cases.append(build(random_ops(rng, 300_000, near=100)))                       # short offsets
+    cases.append(build(random_ops(rng, 600_000, max_off=400_000, near=300_000)))  # copy-4 offsets
     for s, e in cases:
         assert oracle.uncompress(s) == e
-        assert sm.uncompress(s) == e
-        assert sm.last_uncompress_path() == 2
-        assert sm.validate(s) == 0
+        assert sm.uncompress(s) == e, len(e)
+        assert sm.last_uncompress_path() == (4 if small_path(sm, s) else sm.last_uncompress_path())
+    assert sum(small_path(sm, s) for s, _ in cases) >= len(cases) - 12
+    # mutations: the reference's status (its first error), and its output when still valid
+    for f in ("html", "alice29.txt", "urls.10K", "sample-tweet.json", "geo.protodata"):
+        good = sm.compress(read_testfile(f), mode="fast")
+        for _ in range(30):
+            bad = bytearray(good)
+            for _ in range(int(rng.integers(1, 4))):
+                bad[int(rng.integers(2, len(bad)))] = int(rng.integers(0, 256))
+            bad = bytes(bad)
+            st_o, out_o = oracle.uncompress_status(bad)
+            try:
+                st_g, out_g = 0, sm.uncompress(bad)
+            except sm.SnappyError as exc:
+                st_g, out_g = exc.code, None
+            assert st_g == st_o
+            if st_o == 0:
+                assert out_g == out_o
 
 
 def test_host_path_piece_boundaries(sm, oracle, gpu_available):

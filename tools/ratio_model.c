@@ -5,6 +5,8 @@
 // compute: copies up to 255 bytes that stop at the super-chunk end, positions without 4 bytes
 // before the super-chunk end start no copy), literal runs merged inside a super-chunk only, and the
 // block-level fallback to one literal.  Variants (environment):
+//   MARGIN=m   (LONG16) a near (< FAR) recent candidate only when longer than the older by >= m
+//   TBITS=b    hash table of 2^b buckets (kernel: 13)
 //   FAR=d      the older candidate when the recent one is nearer than d (kernel: 256)
 //   LONGEST=1  of the two 4-byte-matching candidates, the one with the longer match (ties: recent)
 //   LONG8=1    ... the longer by an 8-byte compare only (ties and both >= 8: the FAR rule)
@@ -25,10 +27,13 @@ static uint32_t ld32(const uint8_t* p) {
   memcpy(&v, p, 4);
   return v;
 }
-static int far_d = 256, longest = 0, long8 = 0, long16 = 0, xsc = 0, merge = 0, scs = 1024;
+static int margin = 0, tbits = 13, far_d = 256, longest = 0, long8 = 0, long16 = 0, xsc = 0, merge = 0, scs = 1024;
 
 static uint32_t lit_bytes(uint32_t n) { return n == 0 ? 0 : n + (n <= 60 ? 1 : (n <= 256 ? 2 : (n <= 65536 ? 3 : 4))); }
+static uint64_t n_copies = 0, n_near = 0;
 static uint32_t copy_bytes(uint32_t off, uint32_t L) {
+  ++n_copies;
+  n_near += off < 256;
   uint32_t k = L >= 68 ? (L - 4) >> 6 : 0, R0 = L - 64 * k, x = R0 > 64, R = R0 - 60 * x;
   return 3 * (k + x) + ((R < 12 && off < 2048) ? 2 : 3);
 }
@@ -48,7 +53,7 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
     has[q] = 0;
     if (q + 4 > n) continue;
     const uint32_t w = ld32(b + q);
-    const uint32_t h = (w * 0x1e35a7bdu) >> 19;
+    const uint32_t h = (w * 0x1e35a7bdu) >> (32 - tbits);
     const uint32_t par = (q >> 6) & 1;
     const uint32_t own = par ? T[h] >> 16 : T[h] & 0xffff, oth = par ? T[h] & 0xffff : T[h] >> 16;
     T[h] = par ? (T[h] & 0xffff) | ((q + 1) << 16) : (T[h] & 0xffff0000u) | (q + 1);
@@ -61,7 +66,10 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
       const uint32_t cap = long16 ? 16 : 8;
       const uint32_t lim = (long8 || long16) ? (q + cap < n ? q + cap : n) : n;
       const uint32_t l1 = mlen(b, p1, q, lim), l2 = mlen(b, p2, q, lim);
-      if (l1 != l2) use2 = l2 > l1;
+      if (margin && q - p1 < (uint32_t)far_d)  // a near recent one only when longer by >= margin
+        use2 = !(l1 >= l2 + (uint32_t)margin);
+      else if (l1 != l2)
+        use2 = l2 > l1;
       else if (longest) use2 = 0;
     }
     has[q] = 1;
@@ -110,6 +118,8 @@ static uint32_t vlen(uint32_t v) { return v < 128 ? 1 : v < 16384 ? 2 : v < (1u 
 
 int main(int argc, char** argv) {
   if (getenv("FAR")) far_d = atoi(getenv("FAR"));
+  if (getenv("TBITS")) tbits = atoi(getenv("TBITS"));
+  if (getenv("MARGIN")) margin = atoi(getenv("MARGIN"));
   if (getenv("LONGEST")) longest = atoi(getenv("LONGEST"));
   if (getenv("LONG8")) long8 = atoi(getenv("LONG8"));
   if (getenv("LONG16")) long16 = atoi(getenv("LONG16"));
@@ -141,6 +151,6 @@ int main(int argc, char** argv) {
     free(b);
     free(o);
   }
-  printf("worst %.4f  total %.4f\n", worst, tot_m / tot_r);
+  printf("worst %.4f  total %.4f  copies %lu near(<256) %.3f\n", worst, tot_m / tot_r, (unsigned long)n_copies, (double)n_near / n_copies);
   return 0;
 }
