@@ -125,6 +125,7 @@ struct HostTrace {
 constexpr uint32_t kParallelMinOutput = 4 * 65536;  // smaller streams: one wave is as fast
 constexpr size_t kOrgKeep = 256u << 20;  // origin-pointer scratch a context keeps after a decode
 constexpr size_t kPipeMinInput = 32u << 20;  // sm_compress: inputs this large upload in pieces
+constexpr size_t kSmallCompressMax = 4u << 20;  // sm_compress: inputs up to this size synchronise once
 constexpr uint32_t kPieceFrags = 256;        // 16 MiB per piece
 #ifndef SM_OUT_PIECE
 #define SM_OUT_PIECE 2048
@@ -870,6 +871,29 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   uint32_t* d_in_len = (uint32_t*)(m + 24 * (size_t)nfrag);
   uint32_t* d_out_len = (uint32_t*)(m + 28 * (size_t)nfrag);
   HT_DECL
+  // Small inputs: one synchronisation -- the fragment table, the length scan and the gather on
+  // the device, the stream body down into the context's pinned staging (its capacity bound, not
+  // its length, which only the device knows), then copied out on the host.
+  if (n <= kSmallCompressMax && ctx->stage.ensure(sm_max_compressed_length(n) + 16) == hipSuccess) {
+    uint64_t* d_tot = (uint64_t*)(m + 32 * (size_t)nfrag);
+    SM_CHECK(hipMemcpyAsync(ctx->in.p, input, n, hipMemcpyHostToDevice, s));
+    SM_CHECK(sm::launch_frag_plan(n, nfrag, slot, d_in_off, d_in_len, d_out_off, s));
+    sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
+                       nfrag, sm::hashtable_size(n), 0};
+    SM_CHECK(sm::launch_compress(a, mode, s));
+    SM_CHECK(sm::launch_frag_scan_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag, d_dst_off,
+                                         d_tot, (uint8_t*)ctx->out2.p, s));
+    uint64_t tot[2] = {0, 0};
+    SM_CHECK(hipMemcpyAsync(tot, d_tot, 16, hipMemcpyDeviceToHost, s));
+    SM_CHECK(hipMemcpyAsync(ctx->stage.p, ctx->out2.p, sm_max_compressed_length(n) - hl, hipMemcpyDeviceToHost, s));
+    SM_CHECK(hipStreamSynchronize(s));
+    HT("compress (small): all")
+    if (tot[1]) return SM_ERR_DEVICE;  // a block's error mark (SM_OUT_LEN_ERROR), never expected
+    if (hl + tot[0] > *compressed_length) return SM_BUFFER_TOO_SMALL;
+    memcpy(compressed + hl, ctx->stage.p, tot[0]);
+    *compressed_length = hl + tot[0];
+    return SM_OK;
+  }
   SM_CHECK(hipMemcpyAsync(d_in_off, in_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
   SM_CHECK(hipMemcpyAsync(d_out_off, out_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
   SM_CHECK(hipMemcpyAsync(d_in_len, in_len.data(), 4 * (size_t)nfrag, hipMemcpyHostToDevice, s));

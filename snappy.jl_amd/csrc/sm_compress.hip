@@ -387,6 +387,109 @@ __global__ __launch_bounds__(256) void k_gather(const uint8_t* __restrict__ src,
   for (uint32_t k = threadIdx.x; k < n; k += blockDim.x) d[k] = s[k];
 }
 
+// ---- the single-buffer call's device-side bookkeeping (sm_compress, small inputs) ----------
+// Fragment f of the input is [64 KiB f, +64 KiB) and compresses into slot f (fixed pitch).
+__global__ __launch_bounds__(256) void k_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off,
+                                                   uint32_t* in_len, uint64_t* out_off) {
+  const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+  if (f >= nfrag) return;
+  const uint64_t b = (uint64_t)f * kBlockSize;
+  in_off[f] = b;
+  in_len[f] = (uint32_t)min((uint64_t)kBlockSize, n - b);
+  out_off[f] = (uint64_t)f * slot;
+}
+
+// One workgroup: dst_off = exclusive scan of the fragments' lengths, tot[0] = their sum, tot[1]
+// = 1 when a length is an error mark or larger than its fragment's bound (never expected).
+__global__ __launch_bounds__(1024) void k_frag_scan(const uint32_t* out_len, const uint32_t* in_len, uint32_t nfrag,
+                                                    uint64_t* dst_off, uint64_t* tot) {
+  __shared__ uint64_t part[1024 / kWave];
+  __shared__ uint64_t carry;
+  __shared__ uint32_t bad;
+  const uint32_t t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  if (t == 0) {
+    carry = 0;
+    bad = 0;
+  }
+  __syncthreads();
+  for (uint32_t base = 0; base < nfrag; base += 1024) {
+    const uint32_t f = base + t;
+    const uint32_t L = f < nfrag ? out_len[f] : 0u;
+    if (f < nfrag && (uint64_t)L > 32 + (uint64_t)in_len[f] + in_len[f] / 6) atomicOr(&bad, 1u);
+    const uint32_t v = f < nfrag ? L : 0u;
+    const uint32_t incl = scan_dpp(v);  // (a fragment's length < 2^17: wave sums fit u32)
+    if (lane == kWave - 1) part[w] = incl;
+    __syncthreads();
+    uint64_t before = carry;
+    for (uint32_t k = 0; k < w; ++k) before += part[k];
+    if (f < nfrag) dst_off[f] = before + incl - v;
+    __syncthreads();
+    if (t == 1023) carry = before + incl;
+    __syncthreads();
+  }
+  if (t == 0) {
+    tot[0] = carry;
+    tot[1] = bad;
+  }
+}
+
+// Fragment b's len[b] bytes from src + src_off[b] (16-byte aligned) to dst + dst_off[b] (any
+// alignment): aligned 16-byte stores of byte-shifted units, the partial units at both ends by
+// bytes (they share a 16-byte unit with the neighbouring fragments); blockIdx.y strides the units.
+// Nothing when k_frag_scan flagged a length (its offsets are then meaningless).
+__global__ __launch_bounds__(256) void k_gather16(const uint8_t* __restrict__ src, const uint64_t* src_off,
+                                                  const uint32_t* len, const uint64_t* dst_off,
+                                                  const uint64_t* tot, uint8_t* __restrict__ dst) {
+  if (tot[1]) return;
+  const uint32_t b = blockIdx.x;
+  const uint4* s16 = reinterpret_cast<const uint4*>(src + src_off[b]);
+  const uint8_t* s8 = src + src_off[b];
+  uint8_t* const g = dst + dst_off[b];
+  const uint32_t n = len[b];
+  const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
+  const uint32_t u0 = ad ? 1u : 0u, u1 = (n + ad) >> 4;  // whole units [u0, u1); unit u = bytes [16u - ad, +16)
+  uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
+  const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;
+  const uint32_t stride = blockDim.x * gridDim.y;
+  for (uint32_t u = u0 + blockIdx.y * blockDim.x + threadIdx.x; u < u1; u += stride) {
+    const uint32_t j = 16 * u - ad;
+    const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
+    const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    uint32_t r5[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      uint32_t vv = x[q];
+#pragma unroll
+      for (int dd = 1; dd < 4; ++dd) vv = dw == (uint32_t)dd ? x[q + dd] : vv;
+      r5[q] = vv;
+    }
+    g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
+                        __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
+  }
+  if (blockIdx.y == 0) {
+    const uint32_t nh = min(u0 ? 16 - ad : 0u, n);
+    const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);
+    if (threadIdx.x < nh + (n - tb)) {
+      const uint32_t jj = threadIdx.x < nh ? threadIdx.x : tb + (threadIdx.x - nh);
+      g[jj] = s8[jj];
+    }
+  }
+}
+
+hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,
+                            uint64_t* out_off, hipStream_t s) {
+  hipLaunchKernelGGL(k_frag_plan, dim3((nfrag + 255) / 256), dim3(256), 0, s, n, nfrag, slot, in_off, in_len, out_off);
+  return hipGetLastError();
+}
+
+hipError_t launch_frag_scan_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* out_len,
+                                   const uint32_t* in_len, uint32_t nfrag, uint64_t* dst_off, uint64_t* tot,
+                                   uint8_t* dst, hipStream_t s) {
+  hipLaunchKernelGGL(k_frag_scan, dim3(1), dim3(1024), 0, s, out_len, in_len, nfrag, dst_off, tot);
+  hipLaunchKernelGGL(k_gather16, dim3(nfrag, 4), dim3(256), 0, s, src, src_off, out_len, dst_off, tot, dst);
+  return hipGetLastError();
+}
+
 #if SM_STAMP
 extern "C" int sm_debug_stamps_x(unsigned long long* out, int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_x), sizeof(g_stamp_x)) != hipSuccess) return -1;

@@ -80,7 +80,11 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #endif
 // Reads served from the block in HBM/L1 (a raw buffer over [0, n): unaligned, no bank
 // conflicts, the vector-memory pipe instead of the LDS): 1 the candidate checks (C), 2 the walks'
-// position bytes, 4 the walks' candidate bytes (D).
+// position bytes, 4 the walks' candidate bytes (D).  Measured (10K text blocks): 2 removes the
+// position bytes' 4-way bank conflict (row strides of 16 B: 58% of their LDS cycles,
+// profiles/r04_pmc_lds_attribution.json) but gains at most 1.5% (2.49 -> 2.45 ms in one A/B,
+// equal in the next); 1 and 4 put HBM/L1 latency on the walk's dependent chain (2.58 and
+// 2.50 ms).  Default 0: everything from the LDS copy.
 #ifndef SC_GC
 #define SC_GC 0
 #endif
@@ -446,14 +450,14 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
     const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
     if constexpr (kDense) {
-      // dense mode: both candidates compared over 16 bytes, the longer kept (ties: the more
-      // recent), its length stored for the walks
+      // dense mode: both candidates compared over 16 bytes, the longer kept, its length stored
+      // for the walks; on a tie the SC_FAR rule below (the older when the more recent is near)
       const uint4 X = sc_ld128(S.blk, q);
       uint32_t lw1 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p1 & ~3u)), p1 & 3u);
       uint32_t lw2 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p2 & ~3u)), p2 & 3u);
       asm("" : "+v"(lw1), "+v"(lw2));  // (keeps the loads unconditional)
       const uint32_t l1 = ok1 ? lw1 : 0u, l2 = ok2 ? lw2 : 0u;
-      const bool take2 = l2 > l1;
+      const bool take2 = l2 == l1 ? (l2 >= 4 && q - p1 < (uint32_t)SC_FAR) : l2 > l1;
       const uint32_t l = take2 ? l2 : l1;
       const uint32_t avail = sce - q;  // (>= 4 where l >= 4: room)
       const uint32_t enc = l < 4 ? 0u : ((l == 16 && avail > 16) ? kScExt : min(l, avail));
@@ -536,7 +540,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
           } else {
             const uint32_t q = c0 + i, off = offAt(i);
             uint4 X;
-            if (SC_GC & 2) {
+            if ((SC_GC & 2) && q + 16 <= n) {  // (the block's last 15 positions: from the LDS copy)
               const auto v = __builtin_amdgcn_raw_buffer_load_b128(gb, (int)q, 0, 0);
               X = make_uint4(v[0], v[1], v[2], v[3]);
             } else {

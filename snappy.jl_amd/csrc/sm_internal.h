@@ -84,6 +84,15 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
                                uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
                                uint8_t* out, hipStream_t s);
 hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s);
+// sm_compress, small inputs, without host round trips: the fragments' offsets and lengths
+// (fragment f = input [64 KiB f, +64 KiB), output slot f at pitch `slot`); then, after the
+// compress launch, the exclusive scan of the output lengths (tot[0] = total, tot[1] = 1 on a bad
+// length) and the fragments gathered behind one another into dst.
+hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,
+                            uint64_t* out_off, hipStream_t s);
+hipError_t launch_frag_scan_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* out_len,
+                                   const uint32_t* in_len, uint32_t nfrag, uint64_t* dst_off, uint64_t* tot,
+                                   uint8_t* dst, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)
 hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
                          const uint64_t* dst_off, uint8_t* dst, uint32_t nblk, hipStream_t s);

@@ -149,6 +149,27 @@ def test_fast_mode_roundtrip_whole_file(sm, oracle, libsnappy, gpu_available, fn
     assert sm.uncompress(out) == raw
 
 
+# per-file size bounds against the reference's own stream (the oracle = Snappy.jl's parse):
+# dense mode compares both candidates of every copy over 16 bytes, as the reference's extension
+# does for its one candidate (internal.jl:211-239); fast mode takes one by the SC_FAR rule
+SIZE_BOUND = {"dense": 1.01, "fast": 1.04}
+
+
+@pytest.mark.parametrize("mode", FAST_MODES)
+def test_fast_mode_sizes_per_corpus_file(sm, oracle, gpu_available, mode):
+    """every corpus file (test/runtests.jl:8-24 and the benchmark files) is at
+    most SIZE_BOUND[mode] x the reference's stream + 64 B (profiles/r04_fast_sizes.txt)."""
+    files = sorted(set(ROUNDTRIP_FILES + ["sample-tweet.json", "html_x_4"]))
+    worst = 0.0
+    for f in files:
+        raw = read_testfile(f)
+        got, ref = len(sm.compress(raw, mode=mode)), len(oracle.compress(raw))
+        worst = max(worst, got / ref)
+        print("%-18s %s %8d  reference %8d  (%.4f)" % (f, mode, got, ref, got / ref))
+        assert got <= SIZE_BOUND[mode] * ref + 64, (f, got, ref)
+    print("worst %.4f" % worst)
+
+
 @pytest.mark.parametrize("mode", FAST_MODES)
 def test_fast_mode_deterministic(sm, gpu_available, corpus, mode):
     """The parse has no order-dependent state: repeated launches give identical bytes."""

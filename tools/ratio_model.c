@@ -5,6 +5,8 @@
 // compute: copies up to 255 bytes that stop at the super-chunk end, positions without 4 bytes
 // before the super-chunk end start no copy), literal runs merged inside a super-chunk only, and the
 // block-level fallback to one literal.  Variants (environment):
+//   BLK=b      fragment bytes (64 KiB)
+//   LONGNEAR=1 the FAR rule, but a near recent candidate against the older by 16-byte lengths
 //   MARGIN=m   (LONG16) a near (< FAR) recent candidate only when longer than the older by >= m
 //   TBITS=b    hash table of 2^b buckets (kernel: 13)
 //   FAR=d      the older candidate when the recent one is nearer than d (kernel: 256)
@@ -27,10 +29,11 @@ static uint32_t ld32(const uint8_t* p) {
   memcpy(&v, p, 4);
   return v;
 }
-static int margin = 0, tbits = 13, far_d = 256, longest = 0, long8 = 0, long16 = 0, xsc = 0, merge = 0, scs = 1024;
+static int blk = 65536, longnear = 0, margin = 0, tbits = 13, far_d = 256, longest = 0, long8 = 0, long16 = 0, xsc = 0, merge = 0, scs = 1024;
 
 static uint32_t lit_bytes(uint32_t n) { return n == 0 ? 0 : n + (n <= 60 ? 1 : (n <= 256 ? 2 : (n <= 65536 ? 3 : 4))); }
-static uint64_t n_copies = 0, n_near = 0;
+static uint64_t n_copies = 0, n_near = 0, n_both = 0, n_need = 0;
+static uint8_t g_both[65536], g_need[65536];
 static uint32_t copy_bytes(uint32_t off, uint32_t L) {
   ++n_copies;
   n_near += off < 256;
@@ -62,7 +65,12 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
     if (!m1 && !m2) continue;
     const uint32_t p1 = c1 - 1, p2 = c2 - 1;
     int use2 = m2 && (!m1 || q - p1 < (uint32_t)far_d);
-    if (m1 && m2 && (longest || long8 || long16)) {
+    if (longnear && m1 && m2 && q - p1 < (uint32_t)far_d) {  // only a near recent one is compared
+      const uint32_t lim = q + 16 < n ? q + 16 : n;
+      const uint32_t l1 = mlen(b, p1, q, lim), l2 = mlen(b, p2, q, lim);
+      use2 = l2 >= l1;
+    } else if (longnear) {
+    } else if (m1 && m2 && (longest || long8 || long16)) {
       const uint32_t cap = long16 ? 16 : 8;
       const uint32_t lim = (long8 || long16) ? (q + cap < n ? q + cap : n) : n;
       const uint32_t l1 = mlen(b, p1, q, lim), l2 = mlen(b, p2, q, lim);
@@ -74,6 +82,11 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
     }
     has[q] = 1;
     cand[q] = use2 ? p2 : p1;
+    g_both[q] = m1 && m2;
+    {
+      const uint32_t lim16 = q + 16 < n ? q + 16 : n;
+      g_need[q] = m1 && m2 && (mlen(b, p1, q, lim16) < 16 || q - p1 < (uint32_t)far_d);
+    }
   }
   uint64_t out = 0;
   uint32_t run = 0;  // pending literal run
@@ -90,6 +103,8 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
         uint32_t L = mlen(b, cand[p], p, lim);
         if (L > 255) L = 255;
         if (L >= 4) {
+          n_both += g_both[p];
+          n_need += g_need[p];
           out += lit_bytes(run);
           run = 0;
           out += copy_bytes(p - cand[p], L);
@@ -120,6 +135,8 @@ int main(int argc, char** argv) {
   if (getenv("FAR")) far_d = atoi(getenv("FAR"));
   if (getenv("TBITS")) tbits = atoi(getenv("TBITS"));
   if (getenv("MARGIN")) margin = atoi(getenv("MARGIN"));
+  if (getenv("LONGNEAR")) longnear = atoi(getenv("LONGNEAR"));
+  if (getenv("BLK")) blk = atoi(getenv("BLK"));
   if (getenv("LONGEST")) longest = atoi(getenv("LONGEST"));
   if (getenv("LONG8")) long8 = atoi(getenv("LONG8"));
   if (getenv("LONG16")) long16 = atoi(getenv("LONG16"));
@@ -139,7 +156,7 @@ int main(int argc, char** argv) {
     fclose(fp);
     memset(b + sz, 0, 64);
     uint64_t m = vlen((uint32_t)sz);
-    for (long off = 0; off < sz; off += 65536) m += block_bytes(b + off, (uint32_t)(sz - off < 65536 ? sz - off : 65536));
+    for (long off = 0; off < sz; off += blk) m += block_bytes(b + off, (uint32_t)(sz - off < blk ? sz - off : blk));
     size_t r = 0;
     if (smo_compress(b, sz, o, &r, 0) != 0) return 1;
     const double q = (double)m / r;
@@ -151,6 +168,6 @@ int main(int argc, char** argv) {
     free(b);
     free(o);
   }
-  printf("worst %.4f  total %.4f  copies %lu near(<256) %.3f\n", worst, tot_m / tot_r, (unsigned long)n_copies, (double)n_near / n_copies);
+  printf("worst %.4f  total %.4f  copies %lu near(<256) %.3f both %.3f need %.3f\n", worst, tot_m / tot_r, (unsigned long)n_copies, (double)n_near / n_copies, (double)n_both / n_copies, (double)n_need / n_copies);
   return 0;
 }
