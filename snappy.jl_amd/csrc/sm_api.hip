@@ -125,7 +125,7 @@ struct HostTrace {
 constexpr uint32_t kParallelMinOutput = 4 * 65536;  // smaller streams: one wave is as fast
 constexpr size_t kOrgKeep = 256u << 20;  // origin-pointer scratch a context keeps after a decode
 constexpr size_t kPipeMinInput = 32u << 20;  // sm_compress: inputs this large upload in pieces
-constexpr size_t kSmallCompressMax = 4u << 20;  // sm_compress: inputs up to this size synchronise once
+constexpr size_t kSmallCompressMax = 4u << 20;  // sm_compress: inputs up to this size (64 fragments) synchronise once
 constexpr uint32_t kPieceFrags = 256;        // 16 MiB per piece
 #ifndef SM_OUT_PIECE
 #define SM_OUT_PIECE 2048
@@ -370,7 +370,7 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   const uint32_t nchunks = (n - ip0 + kSmallChunk - 1) / kSmallChunk;
   uint32_t rounds = 1;  // kSmallHops^rounds >= size: every chain (at most size steps) resolves
   for (uint64_t reach = sm::kSmallHops; reach < size; reach *= sm::kSmallHops) ++rounds;
-  const size_t path_off = align_up((size_t)nchunks * kIdxEntries * 8, 256);
+  const size_t path_off = align_up((size_t)nchunks * kIdxEntries * 8 + (size_t)nchunks * sm::kDeepLevels * 16, 256);  // records, deep records
   const size_t ctl_off = align_up(path_off + (size_t)nchunks * sizeof(sm::OriginPath), 256);
   const size_t ctl_n = 4 + rounds;
   if (ctx->idx.ensure(ctl_off + ctl_n * 4) != hipSuccess) return 0;
@@ -378,7 +378,6 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   hipStream_t s = ctx->stream;
   uint8_t* ib = (uint8_t*)ctx->idx.p;
   uint32_t* d_ctl = (uint32_t*)(ib + ctl_off);
-  if (hipMemsetAsync(d_ctl, 0, ctl_n * 4, s) != hipSuccess) return -1;
   if (sm::launch_small_decode((const uint8_t*)ctx->in.p, n, ip0, size, nchunks, (uint32_t*)ib,
                               (sm::OriginPath*)(ib + path_off), d_ctl, (uint32_t*)ctx->org.p, rounds,
                               (uint8_t*)ctx->out.p, s) != hipSuccess)
@@ -871,8 +870,8 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   uint32_t* d_in_len = (uint32_t*)(m + 24 * (size_t)nfrag);
   uint32_t* d_out_len = (uint32_t*)(m + 28 * (size_t)nfrag);
   HT_DECL
-  // Small inputs: one synchronisation -- the fragment table, the length scan and the gather on
-  // the device, the stream body down into the context's pinned staging (its capacity bound, not
+  // Small inputs: one synchronisation -- the fragment table and the gather (with the lengths'
+  // prefix sums) on the device, the stream body down into the context's pinned staging (its capacity bound, not
   // its length, which only the device knows), then copied out on the host.
   if (n <= kSmallCompressMax && ctx->stage.ensure(sm_max_compressed_length(n) + 16) == hipSuccess) {
     uint64_t* d_tot = (uint64_t*)(m + 32 * (size_t)nfrag);
@@ -881,8 +880,8 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
     sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
                        nfrag, sm::hashtable_size(n), 0};
     SM_CHECK(sm::launch_compress(a, mode, s));
-    SM_CHECK(sm::launch_frag_scan_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag, d_dst_off,
-                                         d_tot, (uint8_t*)ctx->out2.p, s));
+    SM_CHECK(sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag, d_tot,
+                                    (uint8_t*)ctx->out2.p, s));
     uint64_t tot[2] = {0, 0};
     SM_CHECK(hipMemcpyAsync(tot, d_tot, 16, hipMemcpyDeviceToHost, s));
     SM_CHECK(hipMemcpyAsync(ctx->stage.p, ctx->out2.p, sm_max_compressed_length(n) - hl, hipMemcpyDeviceToHost, s));

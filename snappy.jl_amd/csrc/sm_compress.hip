@@ -399,52 +399,37 @@ __global__ __launch_bounds__(256) void k_frag_plan(uint64_t n, uint32_t nfrag, u
   out_off[f] = (uint64_t)f * slot;
 }
 
-// One workgroup: dst_off = exclusive scan of the fragments' lengths, tot[0] = their sum, tot[1]
-// = 1 when a length is an error mark or larger than its fragment's bound (never expected).
-__global__ __launch_bounds__(1024) void k_frag_scan(const uint32_t* out_len, const uint32_t* in_len, uint32_t nfrag,
-                                                    uint64_t* dst_off, uint64_t* tot) {
-  __shared__ uint64_t part[1024 / kWave];
-  __shared__ uint64_t carry;
-  __shared__ uint32_t bad;
-  const uint32_t t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
-  if (t == 0) {
-    carry = 0;
-    bad = 0;
+// Fragment b's len[b] bytes from src + src_off[b] (16-byte aligned) to dst + (the lengths of
+// fragments 0..b-1, one lane each: nfrag <= 64) at any alignment: aligned 16-byte stores of
+// byte-shifted units, the partial units at both ends by bytes (they share a 16-byte unit with the
+// neighbouring fragments); blockIdx.y strides the units.  tot[0] = the sum, tot[1] = 1 when a
+// length is an error mark or over its fragment's bound (never expected): then nothing is copied.
+__global__ __launch_bounds__(256) void k_gather16(const uint8_t* __restrict__ src, const uint64_t* src_off,
+                                                  const uint32_t* len, const uint32_t* in_len, uint32_t nfrag,
+                                                  uint64_t* tot, uint8_t* __restrict__ dst) {
+  __shared__ uint32_t sh[2];
+  const uint32_t b = blockIdx.x;
+  if (threadIdx.x < kWave) {
+    const uint32_t l = threadIdx.x;
+    const uint32_t L = l < nfrag ? len[l] : 0u;
+    const bool bad = l < nfrag && (uint64_t)L > 32 + (uint64_t)in_len[l] + in_len[l] / 6;
+    const uint32_t before = scan_dpp(l < b ? L : 0u);  // (lanes < b: their lengths; < 2^17 each)
+    const uint32_t all = scan_dpp(bad ? 0u : L);
+    const bool anybad = ballot(bad) != 0;
+    if (l == 63) {
+      sh[0] = before;
+      sh[1] = anybad;
+      if (b == 0 && blockIdx.y == 0) {
+        tot[0] = all;
+        tot[1] = anybad;
+      }
+    }
   }
   __syncthreads();
-  for (uint32_t base = 0; base < nfrag; base += 1024) {
-    const uint32_t f = base + t;
-    const uint32_t L = f < nfrag ? out_len[f] : 0u;
-    if (f < nfrag && (uint64_t)L > 32 + (uint64_t)in_len[f] + in_len[f] / 6) atomicOr(&bad, 1u);
-    const uint32_t v = f < nfrag ? L : 0u;
-    const uint32_t incl = scan_dpp(v);  // (a fragment's length < 2^17: wave sums fit u32)
-    if (lane == kWave - 1) part[w] = incl;
-    __syncthreads();
-    uint64_t before = carry;
-    for (uint32_t k = 0; k < w; ++k) before += part[k];
-    if (f < nfrag) dst_off[f] = before + incl - v;
-    __syncthreads();
-    if (t == 1023) carry = before + incl;
-    __syncthreads();
-  }
-  if (t == 0) {
-    tot[0] = carry;
-    tot[1] = bad;
-  }
-}
-
-// Fragment b's len[b] bytes from src + src_off[b] (16-byte aligned) to dst + dst_off[b] (any
-// alignment): aligned 16-byte stores of byte-shifted units, the partial units at both ends by
-// bytes (they share a 16-byte unit with the neighbouring fragments); blockIdx.y strides the units.
-// Nothing when k_frag_scan flagged a length (its offsets are then meaningless).
-__global__ __launch_bounds__(256) void k_gather16(const uint8_t* __restrict__ src, const uint64_t* src_off,
-                                                  const uint32_t* len, const uint64_t* dst_off,
-                                                  const uint64_t* tot, uint8_t* __restrict__ dst) {
-  if (tot[1]) return;
-  const uint32_t b = blockIdx.x;
+  if (sh[1]) return;
   const uint4* s16 = reinterpret_cast<const uint4*>(src + src_off[b]);
   const uint8_t* s8 = src + src_off[b];
-  uint8_t* const g = dst + dst_off[b];
+  uint8_t* const g = dst + sh[0];
   const uint32_t n = len[b];
   const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
   const uint32_t u0 = ad ? 1u : 0u, u1 = (n + ad) >> 4;  // whole units [u0, u1); unit u = bytes [16u - ad, +16)
@@ -482,11 +467,10 @@ hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t*
   return hipGetLastError();
 }
 
-hipError_t launch_frag_scan_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* out_len,
-                                   const uint32_t* in_len, uint32_t nfrag, uint64_t* dst_off, uint64_t* tot,
-                                   uint8_t* dst, hipStream_t s) {
-  hipLaunchKernelGGL(k_frag_scan, dim3(1), dim3(1024), 0, s, out_len, in_len, nfrag, dst_off, tot);
-  hipLaunchKernelGGL(k_gather16, dim3(nfrag, 4), dim3(256), 0, s, src, src_off, out_len, dst_off, tot, dst);
+hipError_t launch_frag_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* out_len,
+                              const uint32_t* in_len, uint32_t nfrag, uint64_t* tot, uint8_t* dst, hipStream_t s) {
+  if (nfrag == 0 || nfrag > kWave) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gather16, dim3(nfrag, 4), dim3(256), 0, s, src, src_off, out_len, in_len, nfrag, tot, dst);
   return hipGetLastError();
 }
 

@@ -717,9 +717,58 @@ __device__ inline uint32_t window_tags(const uint8_t* buf, uint32_t rel0, uint32
   return ntok;
 }
 
-template <uint32_t kC>  // compressed bytes per chunk (kIdxChunk; path 4: kSmallChunk)
+__device__ inline uint64_t load8z(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
+  return (uint64_t)load_word(in, N, p) | ((uint64_t)load_word(in, N, p + 4) << 32);
+}
+
+// Host tag walk (sm_api.hip host_walk) by one wave: where the tags from p leave [p, lim) and
+// their output -- for chunk entries deeper than the index covers.  A 256-byte window of tags per
+// step (walk_window, as k_origin_fill), a literal too long for a window by itself.
+__device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint64_t p, uint64_t lim, uint16_t* jt,
+                                uint32_t lane, uint64_t& exit_pos, uint64_t& produced) {
+  uint64_t o = 0;
+  while (p < lim) {
+    const uint32_t rlim = (uint32_t)min((uint64_t)256, lim - p);
+    uint32_t cpos, csz, sizes;
+    const uint32_t ntok = walk_window(load8z(in, N, (uint32_t)p + 4 * lane), rlim, jt, lane, cpos, csz, sizes);
+    if (ntok == 0) {  // a literal too long for a window walk (or a wrapped length)
+      const uint64_t hv = load8z(in, N, (uint32_t)p);
+      const uint32_t c = uniform((uint32_t)hv & 0xff);
+      const uint32_t entry = char_entry(c);
+      const uint32_t taglen = entry >> 11;
+      const uint32_t tr = uniform((uint32_t)(hv >> 8));
+      const uint32_t trailer = taglen >= 4 ? tr : (tr & ((1u << (8 * taglen)) - 1u));
+      if (c & 3) {
+        p += 1 + taglen;
+        o += entry & 0xff;
+      } else {
+        const uint32_t lit = (entry & 0xff) + trailer;  // u32 wrap, as the reference
+        p += 1ull + taglen + lit;
+        o += lit;
+      }
+      continue;
+    }
+    const bool mine = lane < ntok;
+    const uint32_t c = (uint32_t)load8z(in, N, (uint32_t)p + (mine ? cpos : 0u)) & 0xff;
+    const uint32_t e = char_entry(c);
+    const uint32_t ob = !mine ? 0u : (c & 3) ? (e & 0xff) : csz - 1 - (e >> 11);  // a window literal: csz = 1 + taglen + len
+    const uint32_t incl = scan_dpp(ob);
+    o += readlane(incl, ntok - 1);
+    p += readlane(cpos + csz, ntok - 1);
+  }
+  exit_pos = p;
+  produced = o;
+}
+
+// kDeep (path 4): also deep[kDeepLevels c] = (x, exit, output, 1) for entering the chunk where
+// lane 0's path leaves this one, x, when x lies kIdxEntries or more bytes into it (a long literal
+// across the boundary): the entry the device chain needs there whenever its walk merged with
+// lane 0's path here (then its exit is x).  Level k + 1 likewise enters where level k's walk
+// leaves (consecutive long literals: the chunks between start inside a literal, and their own
+// lane-0 paths need not be the stream's).  .w = 0: no such level.
+template <uint32_t kC, bool kDeep>  // compressed bytes per chunk (kIdxChunk; path 4: kSmallChunk)
 __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
-                                                     uint2* rec) {
+                                                     uint2* rec, uint4* deep) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kC + kIdxPad];
   __shared__ __attribute__((aligned(16))) uint16_t jt[6 * 256];  // walk tables, then the entry walk's 3 KiB
   __shared__ uint32_t bm[kC / 32];  // positions on lane 0's path
@@ -834,6 +883,26 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
   }
   // (exit, output) pairs side by side: the host's walk over the records reads one cache line
   rec[c * kIdxEntries + lane] = make_uint2((uint32_t)min(ex, (uint64_t)0xffffffffu), res);
+  if constexpr (kDeep) {
+    uint64_t x = exit0;
+    for (uint32_t k = 0; k < kDeepLevels; ++k) {
+      const uint64_t dl = (x - ip0) / kC, db = ip0 + dl * kC;
+      uint4 dr = make_uint4(0, 0, 0, 0);
+      if (x < (uint64_t)N - 1 && x - db >= kIdxEntries) {
+        uint64_t dex, dot;
+        dev_walk(in, N, x, min(db + kC, (uint64_t)N - 1), jt, lane, dex, dot);
+        dr = make_uint4((uint32_t)x, (uint32_t)min(dex, (uint64_t)0xffffffffu),
+                        (uint32_t)min(dot, (uint64_t)0xffffffffu), 1u);
+        x = dex;
+      }
+      if (lane == 0) deep[kDeepLevels * c + k] = dr;
+      if (!dr.w) {
+        for (uint32_t j = k + 1; j < kDeepLevels; ++j)
+          if (lane == 0) deep[kDeepLevels * c + j] = make_uint4(0, 0, 0, 0);
+        break;
+      }
+    }
+  }
 }
 
 __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
@@ -999,9 +1068,6 @@ hipError_t launch_uncompressed_length(const uint8_t* in, const uint64_t* in_off,
 // stream (incremental_copy_slow!, internal.jl:477-481).  Any check that fails sends the caller
 // to the in-order decode, which returns the reference's exact status.
 
-__device__ inline uint64_t load8z(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
-  return (uint64_t)load_word(in, N, p) | ((uint64_t)load_word(in, N, p + 4) << 32);
-}
 
 // One path element's tags by one wave (window walks, internal.jl:411-466), with the reference's
 // checks; kFill: the origin pointer of every output byte into P.  Returns the element's status.
@@ -1128,43 +1194,30 @@ __global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ 
 constexpr uint32_t kChainLds = 256;  // chunks whose records the chain reads from LDS (128 KiB)
 constexpr uint32_t kFillStage = kSmallChunk + kIdxPad + 256;  // an element's tags and a window past them
 
-// Host tag walk (sm_api.hip host_walk) by one wave, uniform: where the tags from p leave [p, lim)
-// and their output.  For chunk entries deeper than the index covers.
-__device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint64_t p, uint64_t lim, uint64_t& exit_pos,
-                                uint64_t& produced) {
-  uint64_t o = 0;
-  while (p < lim) {
-    const uint64_t hv = load8z(in, N, (uint32_t)p);
-    const uint32_t c = uniform((uint32_t)hv & 0xff);
-    const uint32_t entry = char_entry(c);
-    const uint32_t taglen = entry >> 11;
-    const uint32_t tr = uniform((uint32_t)(hv >> 8));
-    const uint32_t trailer = taglen >= 4 ? tr : (tr & ((1u << (8 * taglen)) - 1u));
-    if (c & 3) {
-      p += 1 + taglen;
-      o += entry & 0xff;
-    } else {
-      const uint32_t lit = (entry & 0xff) + trailer;  // u32 wrap, as the reference
-      p += 1ull + taglen + lit;
-      o += lit;
-    }
-  }
-  exit_pos = p;
-  produced = o;
-}
-
 // ctl[0] = path elements, ctl[1] = 0 (the path covers exactly `size` bytes of output) or 1 (fall back)
 __global__ __launch_bounds__(64) void k_stream_chain(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
                                                      uint32_t size, uint32_t nchunks, const uint2* __restrict__ rec,
-                                                     OriginPath* path, uint32_t* ctl) {
+                                                     const uint4* __restrict__ deep, OriginPath* path, uint32_t* ctl,
+                                                     uint32_t nrounds) {
   __shared__ uint2 srec[kChainLds * kIdxEntries];
+  __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
   const uint32_t lane = lane_id();
   const bool inlds = nchunks <= kChainLds;
-  if (inlds)
-    for (uint32_t k = lane; k < nchunks * kIdxEntries; k += kWave) srec[k] = rec[k];
+  if (inlds) {  // (eight loads in flight per lane)
+    const uint32_t nr = nchunks * kIdxEntries;
+    for (uint32_t k0 = lane; k0 < nr; k0 += 8 * kWave) {
+      uint2 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = k0 + u * kWave < nr ? rec[k0 + u * kWave] : make_uint2(0, 0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k0 + u * kWave < nr) srec[k0 + u * kWave] = v[u];
+    }
+  }
   __syncthreads();
   uint64_t y = ip0, O = 0;
-  uint32_t np = 0, bad = 0;
+  uint32_t np = 0, bad = 0, cprev = 0xffffffffu;  // the chunk of the previous element
+  uint32_t dsrc = 0xffffffffu, dlev = 0;          // the deep record the previous element came from
   while (y < (uint64_t)N - 1) {  // internal.jl:416
     const uint32_t c = (uint32_t)((y - ip0) / kSmallChunk);
     const uint64_t base = ip0 + (uint64_t)c * kSmallChunk, l = y - base;
@@ -1174,8 +1227,36 @@ __global__ __launch_bounds__(64) void k_stream_chain(const uint8_t* __restrict__
       ex = uniform(r.x);
       ot = uniform(r.y);
     } else {
-      dev_walk(in, N, y, min(base + kSmallChunk, (uint64_t)N - 1), ex, ot);
+      // the next level of the deep record the previous element came from, else level 0 of the
+      // previous element's chunk (it left where that chunk's lane-0 path does), else a walk
+      auto get = [&](uint32_t i) {
+        const uint4 v = deep[i];
+        return make_uint4(uniform(v.x), uniform(v.y), uniform(v.z), uniform(v.w));
+      };
+      uint4 dr = make_uint4(0, 0, 0, 0);
+      uint32_t nsrc = 0xffffffffu, nlev = 0;
+      if (dsrc != 0xffffffffu && dlev + 1 < kDeepLevels) {
+        dr = get(kDeepLevels * dsrc + dlev + 1);
+        nsrc = dsrc;
+        nlev = dlev + 1;
+      }
+      if (!(dr.w && dr.x == y) && cprev != 0xffffffffu) {
+        dr = get(kDeepLevels * cprev);
+        nsrc = cprev;
+        nlev = 0;
+      }
+      if (dr.w && dr.x == y) {
+        ex = dr.y;
+        ot = dr.z;
+        dsrc = nsrc;
+        dlev = nlev;
+      } else {
+        dev_walk(in, N, y, min(base + kSmallChunk, (uint64_t)N - 1), jt, lane, ex, ot);
+        dsrc = 0xffffffffu;
+      }
     }
+    if (l < kIdxEntries) dsrc = 0xffffffffu;
+    cprev = c;
     if (np >= nchunks || ex <= y) {  // (never for a well-formed index: every element leaves its chunk)
       bad = 1;
       break;
@@ -1195,6 +1276,7 @@ __global__ __launch_bounds__(64) void k_stream_chain(const uint8_t* __restrict__
     ctl[0] = np;
     ctl[1] = bad;
   }
+  if (lane >= 2 && lane < 4 + nrounds) ctl[lane] = 0;  // the fill's flag and the resolve counters
 }
 
 // k_origin_fill for the device chain's path: elements past ctl[0] exit; a failing element sets ctl[2]
@@ -1275,10 +1357,12 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
 hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
                                uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
                                uint8_t* out, hipStream_t s) {
-  if (nchunks == 0 || size == 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_stream_index<kSmallChunk>, dim3(nchunks), dim3(64), 0, s, in, N, ip0, reinterpret_cast<uint2*>(rec));
+  if (nchunks == 0 || size == 0 || rounds == 0 || 4 + rounds > kWave) return hipErrorInvalidValue;
+  uint4* deep = reinterpret_cast<uint4*>(rec + (size_t)nchunks * kIdxEntries * 2);  // kDeepLevels per chunk
+  hipLaunchKernelGGL((k_stream_index<kSmallChunk, true>), dim3(nchunks), dim3(64), 0, s, in, N, ip0,
+                     reinterpret_cast<uint2*>(rec), deep);
   hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(64), 0, s, in, N, ip0, size, nchunks,
-                     reinterpret_cast<const uint2*>(rec), path, ctl);
+                     reinterpret_cast<const uint2*>(rec), deep, path, ctl, rounds);
   hipLaunchKernelGGL(k_origin_fill_dev, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
   for (uint32_t r = 0; r < rounds; ++r)
     hipLaunchKernelGGL(k_origin_resolve_hops, dim3(origin_grid(size)), dim3(256), 0, s, P, size, ctl + 4, r);
@@ -1295,7 +1379,8 @@ hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t s
 hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t nchunks, uint32_t* rec,
                                hipStream_t s) {
   if (nchunks == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_stream_index<kIdxChunk>, dim3(nchunks), dim3(64), 0, s, in, N, ip0, reinterpret_cast<uint2*>(rec));
+  hipLaunchKernelGGL((k_stream_index<kIdxChunk, false>), dim3(nchunks), dim3(64), 0, s, in, N, ip0,
+                     reinterpret_cast<uint2*>(rec), nullptr);
   return hipGetLastError();
 }
 

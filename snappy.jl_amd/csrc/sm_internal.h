@@ -45,7 +45,8 @@ hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 constexpr uint32_t kIdxChunk = 4096;  // compressed bytes per index chunk
 constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
 constexpr uint32_t kSmallChunk = 1024;  // path 4 (a small stream on the device): bytes per index chunk
-constexpr uint32_t kSmallHops = 32;     // path 4: chain steps per pointer per resolve launch
+constexpr uint32_t kSmallHops = 64;     // path 4: chain steps per pointer per resolve launch
+constexpr uint32_t kDeepLevels = 4;     // path 4: deep-entry records per chunk (consecutive long literals)
 constexpr uint32_t kIdxPad = 288;     // staged bytes past a chunk: +16 entry slack, a 256-byte walk window + 16
 struct StreamFrag {
   uint32_t y;    // a true tag start at or before the fragment's first tag (chunk entry)
@@ -76,23 +77,23 @@ hipError_t launch_path_check(const uint8_t* in, uint32_t N, uint32_t size, const
                              int32_t* status, hipStream_t s);
 hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, hipStream_t s);
 // A small stream entirely on the device (index, chain, fill, `rounds` resolve launches, gather; no
-// host synchronisation).  rec: nchunks * kIdxEntries u32 pairs; path: nchunks elements; ctl: 4 +
-// rounds zeroed u32 -- ctl[0] path elements, ctl[1] != 0: the chain found no exact path (fall
+// host synchronisation).  rec: nchunks * kIdxEntries u32 pairs, then nchunks * kDeepLevels
+// 16-byte deep-entry records; path: nchunks elements; ctl: 4 +
+// rounds u32 (zeroed by the chain kernel) -- ctl[0] path elements, ctl[1] != 0: the chain found no exact path (fall
 // back), ctl[2] != 0: an element failed its checks (fall back), ctl[4 + r] != 0: pointers still
 // unresolved after round r.  P: size u32.
 hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
                                uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
                                uint8_t* out, hipStream_t s);
 hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s);
-// sm_compress, small inputs, without host round trips: the fragments' offsets and lengths
-// (fragment f = input [64 KiB f, +64 KiB), output slot f at pitch `slot`); then, after the
-// compress launch, the exclusive scan of the output lengths (tot[0] = total, tot[1] = 1 on a bad
-// length) and the fragments gathered behind one another into dst.
+// sm_compress, small inputs (at most 64 fragments), without host round trips: the fragments'
+// offsets and lengths (fragment f = input [64 KiB f, +64 KiB), output slot f at pitch `slot`);
+// then, after the compress launch, the fragments gathered behind one another into dst (tot[0] =
+// their total length, tot[1] = 1 on a bad length, when nothing is copied).
 hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,
                             uint64_t* out_off, hipStream_t s);
-hipError_t launch_frag_scan_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* out_len,
-                                   const uint32_t* in_len, uint32_t nfrag, uint64_t* dst_off, uint64_t* tot,
-                                   uint8_t* dst, hipStream_t s);
+hipError_t launch_frag_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* out_len,
+                              const uint32_t* in_len, uint32_t nfrag, uint64_t* tot, uint8_t* dst, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)
 hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
                          const uint64_t* dst_off, uint8_t* dst, uint32_t nblk, hipStream_t s);

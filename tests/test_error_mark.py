@@ -55,9 +55,10 @@ def test_batch_host_api_reports_device_error(sm, spin0):
     assert not out.any()
 
 
-def test_single_buffer_api_reports_device_error(sm, spin0):
+@pytest.mark.parametrize("nblocks", [8, 65])  # the one-synchronisation path (<= 4 MiB) and the other
+def test_single_buffer_api_reports_device_error(sm, spin0, nblocks):
     L, ctx = spin0
-    raw = np.frombuffer(b"".join(_text_blocks(8)), dtype=np.uint8)
+    raw = np.frombuffer(b"".join(_text_blocks(nblocks)), dtype=np.uint8)
     cap = sm.maxlength_compressed(raw.size)
     out = np.zeros(cap, dtype=np.uint8)
     ol = ctypes.c_size_t(cap)
