@@ -722,17 +722,26 @@ __device__ inline uint64_t load8z(const uint8_t* __restrict__ in, uint32_t N, ui
 }
 
 // Host tag walk (sm_api.hip host_walk) by one wave: where the tags from p leave [p, lim) and
-// their output -- for chunk entries deeper than the index covers.  A 256-byte window of tags per
-// step (walk_window, as k_origin_fill), a literal too long for a window by itself.
+// their output -- for chunk entries deeper than the index covers (lim - p <= kSmallChunk).  The
+// bytes [p, lim + 256 + 32) are staged in stg (LDS, kDevWalkStage bytes) first; a 256-byte
+// window of tags per step (walk_window, as k_origin_fill), a literal too long for a window by
+// itself (its far end read from HBM).
+constexpr uint32_t kDevWalkStage = kSmallChunk + kIdxPad;
 __device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint64_t p, uint64_t lim, uint16_t* jt,
-                                uint32_t lane, uint64_t& exit_pos, uint64_t& produced) {
+                                uint32_t lane, uint8_t* stg, uint64_t& exit_pos, uint64_t& produced) {
+  const uint64_t sp = p;
+  stage_bytes(stg, in, N, (uint32_t)sp, kDevWalkStage, lane);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: its LDS stores land before its loads)
+  auto rd8 = [&](uint64_t x) -> uint64_t {
+    return x >= sp && x - sp + 8 <= kDevWalkStage ? lds_ld64(stg, (uint32_t)(x - sp)) : load8z(in, N, (uint32_t)x);
+  };
   uint64_t o = 0;
   while (p < lim) {
     const uint32_t rlim = (uint32_t)min((uint64_t)256, lim - p);
     uint32_t cpos, csz, sizes;
-    const uint32_t ntok = walk_window(load8z(in, N, (uint32_t)p + 4 * lane), rlim, jt, lane, cpos, csz, sizes);
+    const uint32_t ntok = walk_window(rd8(p + 4 * lane), rlim, jt, lane, cpos, csz, sizes);
     if (ntok == 0) {  // a literal too long for a window walk (or a wrapped length)
-      const uint64_t hv = load8z(in, N, (uint32_t)p);
+      const uint64_t hv = rd8(p);
       const uint32_t c = uniform((uint32_t)hv & 0xff);
       const uint32_t entry = char_entry(c);
       const uint32_t taglen = entry >> 11;
@@ -749,7 +758,7 @@ __device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint
       continue;
     }
     const bool mine = lane < ntok;
-    const uint32_t c = (uint32_t)load8z(in, N, (uint32_t)p + (mine ? cpos : 0u)) & 0xff;
+    const uint32_t c = (uint32_t)rd8(p + (mine ? cpos : 0u)) & 0xff;
     const uint32_t e = char_entry(c);
     const uint32_t ob = !mine ? 0u : (c & 3) ? (e & 0xff) : csz - 1 - (e >> 11);  // a window literal: csz = 1 + taglen + len
     const uint32_t incl = scan_dpp(ob);
@@ -890,7 +899,7 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
       uint4 dr = make_uint4(0, 0, 0, 0);
       if (x < (uint64_t)N - 1 && x - db >= kIdxEntries) {
         uint64_t dex, dot;
-        dev_walk(in, N, x, min(db + kC, (uint64_t)N - 1), jt, lane, dex, dot);
+        dev_walk(in, N, x, min(db + kC, (uint64_t)N - 1), jt, lane, buf, dex, dot);  // (buf: free now)
         dr = make_uint4((uint32_t)x, (uint32_t)min(dex, (uint64_t)0xffffffffu),
                         (uint32_t)min(dot, (uint64_t)0xffffffffu), 1u);
         x = dex;
@@ -1201,6 +1210,7 @@ __global__ __launch_bounds__(64) void k_stream_chain(const uint8_t* __restrict__
                                                      uint32_t nrounds) {
   __shared__ uint2 srec[kChainLds * kIdxEntries];
   __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
+  __shared__ __attribute__((aligned(16))) uint8_t stg[kDevWalkStage + 16];
   const uint32_t lane = lane_id();
   const bool inlds = nchunks <= kChainLds;
   if (inlds) {  // (eight loads in flight per lane)
@@ -1251,7 +1261,7 @@ __global__ __launch_bounds__(64) void k_stream_chain(const uint8_t* __restrict__
         dsrc = nsrc;
         dlev = nlev;
       } else {
-        dev_walk(in, N, y, min(base + kSmallChunk, (uint64_t)N - 1), jt, lane, ex, ot);
+        dev_walk(in, N, y, min(base + kSmallChunk, (uint64_t)N - 1), jt, lane, stg, ex, ot);
         dsrc = 0xffffffffu;
       }
     }

@@ -649,6 +649,16 @@ def test_uncompress_small_streams_device_path(sm, oracle, libsnappy, gpu_availab
     cases.append(build([("lit", b"ab")] + [("copy", 2, 64)] * 4000))             # one period-2 run
     cases.append(build([("lit", b"q")] + [("copy", 1, 1)] * 20_000))             # 1-byte copies
     cases.append(build(random_ops(rng, 300_000, near=100)))                       # short offsets
+    # long literals across index chunks, up to six in a row (deep chunk entries, deep-record
+    # levels 0-3 and the walk past them), between runs of short copies
+    ops = [("lit", rng.integers(0, 256, 50, dtype=np.uint8).tobytes())]
+    for _ in range(120):
+        for _ in range(int(rng.integers(1, 7))):
+            ops.append(("lit", rng.integers(0, 256, int(rng.integers(70, 3000)), dtype=np.uint8).tobytes()))
+        for _ in range(int(rng.integers(40, 160))):
+            ops.append(("copy", int(rng.integers(1, 2000)), int(rng.integers(4, 65))))
+    cases.append(build(ops))
+    assert small_path(sm, cases[-1][0])
     cases.append(build(random_ops(rng, 600_000, max_off=400_000, near=300_000)))  # copy-4 offsets
     for s, e in cases:
         assert oracle.uncompress(s) == e
