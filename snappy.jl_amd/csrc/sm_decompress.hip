@@ -612,8 +612,8 @@ __global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a)
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
   __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];  // tag-walk jump tables
   __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];                // output window
-  const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
+  const uint32_t b = blockIdx.x;
   const uint8_t* in = a.in + a.in_off[b];
   const uint32_t N = a.in_len[b];
   uint8_t* dst = a.out + a.out_off[b];

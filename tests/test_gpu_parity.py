@@ -651,12 +651,14 @@ def test_uncompress_small_streams_device_path(sm, oracle, libsnappy, gpu_availab
     cases.append(build(random_ops(rng, 300_000, near=100)))                       # short offsets
     # long literals across index chunks, up to six in a row (deep chunk entries, deep-record
     # levels 0-3 and the walk past them), between runs of short copies
-    ops = [("lit", rng.integers(0, 256, 50, dtype=np.uint8).tobytes())]
+    ops, size = [("lit", rng.integers(0, 256, 50, dtype=np.uint8).tobytes())], 50
     for _ in range(120):
         for _ in range(int(rng.integers(1, 7))):
             ops.append(("lit", rng.integers(0, 256, int(rng.integers(70, 3000)), dtype=np.uint8).tobytes()))
+            size += len(ops[-1][1])
         for _ in range(int(rng.integers(40, 160))):
-            ops.append(("copy", int(rng.integers(1, 2000)), int(rng.integers(4, 65))))
+            ops.append(("copy", int(rng.integers(1, min(2000, size) + 1)), int(rng.integers(4, 65))))
+            size += ops[-1][2]
     cases.append(build(ops))
     assert small_path(sm, cases[-1][0])
     cases.append(build(random_ops(rng, 600_000, max_off=400_000, near=300_000)))  # copy-4 offsets

@@ -5,6 +5,7 @@
 // compute: copies up to 255 bytes that stop at the super-chunk end, positions without 4 bytes
 // before the super-chunk end start no copy), literal runs merged inside a super-chunk only, and the
 // block-level fallback to one literal.  Variants (environment):
+//   FARMAX=x   ... and the older one is nearer than x
 //   BLK=b      fragment bytes (64 KiB)
 //   LONGNEAR=1 the FAR rule, but a near recent candidate against the older by 16-byte lengths
 //   MARGIN=m   (LONG16) a near (< FAR) recent candidate only when longer than the older by >= m
@@ -29,7 +30,7 @@ static uint32_t ld32(const uint8_t* p) {
   memcpy(&v, p, 4);
   return v;
 }
-static int blk = 65536, longnear = 0, margin = 0, tbits = 13, far_d = 256, longest = 0, long8 = 0, long16 = 0, xsc = 0, merge = 0, scs = 1024;
+static int farmax = 1 << 30, blk = 65536, longnear = 0, margin = 0, tbits = 13, far_d = 256, longest = 0, long8 = 0, long16 = 0, xsc = 0, merge = 0, scs = 1024;
 
 static uint32_t lit_bytes(uint32_t n) { return n == 0 ? 0 : n + (n <= 60 ? 1 : (n <= 256 ? 2 : (n <= 65536 ? 3 : 4))); }
 static uint64_t n_copies = 0, n_near = 0, n_both = 0, n_need = 0;
@@ -64,7 +65,7 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
     const int m1 = c1 && ld32(b + c1 - 1) == w, m2 = c2 && ld32(b + c2 - 1) == w;
     if (!m1 && !m2) continue;
     const uint32_t p1 = c1 - 1, p2 = c2 - 1;
-    int use2 = m2 && (!m1 || q - p1 < (uint32_t)far_d);
+    int use2 = m2 && (!m1 || (q - p1 < (uint32_t)far_d && q - p2 < (uint32_t)farmax));
     if (longnear && m1 && m2 && q - p1 < (uint32_t)far_d) {  // only a near recent one is compared
       const uint32_t lim = q + 16 < n ? q + 16 : n;
       const uint32_t l1 = mlen(b, p1, q, lim), l2 = mlen(b, p2, q, lim);
@@ -137,6 +138,7 @@ int main(int argc, char** argv) {
   if (getenv("MARGIN")) margin = atoi(getenv("MARGIN"));
   if (getenv("LONGNEAR")) longnear = atoi(getenv("LONGNEAR"));
   if (getenv("BLK")) blk = atoi(getenv("BLK"));
+  if (getenv("FARMAX")) farmax = atoi(getenv("FARMAX"));
   if (getenv("LONGEST")) longest = atoi(getenv("LONGEST"));
   if (getenv("LONG8")) long8 = atoi(getenv("LONG8"));
   if (getenv("LONG16")) long16 = atoi(getenv("LONG16"));
