@@ -541,8 +541,8 @@ def test_config5_large_stream(sm, oracle, gpu_available):
 def test_config5_corrupted_stream_first_error(sm, oracle, gpu_available):
     """a corrupted config-5 stream (644 MiB, bytes flipped at 10 seeded
     positions) returns the oracle's status -- the first error in stream order, found by per-tag
-    checks over the tag path in parallel -- in well under half a second (the in-order decode
-    took about a minute)."""
+    checks over the tag path in parallel (path 3; 18-33 ms of GPU work, the call well under a
+    second with its upload) instead of the in-order decode's minute."""
     import time
     sys_path_root()
     import bench
@@ -566,7 +566,9 @@ def test_config5_corrupted_stream_first_error(sm, oracle, gpu_available):
         assert st_g == st_o, (trial, st_g, st_o)
         if st_o != 0:
             assert sm.last_uncompress_path() == 3
-            assert dt < 0.5, dt
+            # (the time includes the ~370 MB pageable upload; the in-order decode took about a
+            # minute, so a generous bound still tells the paths apart -- ADVICE round 3)
+            assert dt < 5.0, dt
         print("trial %d: status %d in %.3f s (path %d)" % (trial, st_g, dt, sm.last_uncompress_path()))
 
 
