@@ -9,11 +9,14 @@
 #include <string.h>
 static uint32_t ld32(const uint8_t* p){uint32_t v;memcpy(&v,p,4);return v;}
 static uint32_t T[8192], T2[8192], cand[65536];
+static long spec_lens, spec_iters;
+static int OV;
 static long n_sc, walk_iters1, rs_rounds, rs_iters, rs_lenlanes, rs_lanes_chg, first_lens, rs_lens, rs_rounds_needlen;
 static int lenAt(const uint8_t* d, uint32_t q, uint32_t sce, uint32_t* enc){
   uint32_t c=cand[q]; uint32_t l=0; while(l<16 && d[c+l]==d[q+l]) ++l;
   uint32_t av=sce-q; *enc = (l==16 && av>16)?17:(l<av?l:av); return 0;}
 int main(int argc,char**argv){
+  if(getenv("OV")) OV=atoi(getenv("OV"));
   for(int f=1;f<argc;++f){FILE*fp=fopen(argv[f],"rb");fseek(fp,0,SEEK_END);long sz=ftell(fp);fseek(fp,0,SEEK_SET);
   uint8_t*d=calloc(sz+64,1);if(fread(d,1,sz,fp)!=(size_t)sz) return 2;fclose(fp);
   for(long o=0;o<sz;o+=65536){uint32_t n=sz-o<65536?sz-o:65536; const uint8_t*b=d+o;
@@ -35,9 +38,21 @@ int main(int argc,char**argv){
         while(i<16){ if(((stop)>>i)&1){mpos=i;break;} path|=1u<<i; last=i; uint32_t enc; lenAt(b,c0+i,sce,&enc); steps++; lastL=enc; \
           uint32_t t=i+(enc<16?enc:16); uint32_t m=mask[l]>>t; i=m?t+__builtin_ctz(m):16; } \
         pend=ce; if(last<16){uint32_t L=lastL; if(last+(L<16?L:16)>=16){ if(L==17){uint32_t q=c0+last,c=cand[q];L=16;uint32_t cap=sce-q<255?sce-q:255;while(L<cap&&b[c+L]==b[q+L])++L;} pend=c0+last+L;}} }
-      int mx=0;
-      for(int l=0;l<64;++l){uint32_t c0=sc0+16*l; uint32_t mp,st; S[l]=c0; if(c0<sce){WALK(l,0,0,P[l],mp,E[l],st);} else {P[l]=0;E[l]=c0;st=0;} first_lens+=st; if((int)st>mx)mx=st;}
-      walk_iters1+=mx;
+      int mx=0, mx0=0;
+      for(int l=0;l<64;++l){uint32_t c0=sc0+16*l; uint32_t mp,st; uint32_t s0=c0, st0=0;
+        if(OV && l>0 && c0<sce){  // speculative entry: walk the previous row from OV bytes before
+          uint32_t pr=l-1, pc0=sc0+16*pr; uint32_t i=16-OV; uint32_t m0=mask[pr]>>i; i=m0?i+__builtin_ctz(m0):16;
+          uint32_t pos=pc0+i;
+          while(i<16){ uint32_t enc; lenAt(b,pc0+i,sce,&enc); st0++; uint32_t L=enc;
+            if(L==17){uint32_t q=pc0+i,c=cand[q];L=16;uint32_t cap=sce-q<255?sce-q:255;while(L<cap&&b[c+L]==b[q+L])++L;}
+            uint32_t t=i+L; if(t>=16){pos=pc0+t;break;} uint32_t m=mask[pr]>>t; i=m?t+__builtin_ctz(m):16; pos=pc0+i; }
+          if(pos<c0) pos=c0;
+          s0=pos; }
+        spec_lens+=st0; if((int)st0>mx0) mx0=st0;
+        S[l]=s0;
+        if(s0<(c0+16<sce?c0+16:sce)){WALK(l,s0-c0,0,P[l],mp,E[l],st);} else {P[l]=0;E[l]=s0;st=0;}
+        first_lens+=st; if((int)st>mx)mx=st;}
+      walk_iters1+=mx; spec_iters+=mx0;
       for(;;){ uint32_t sn[64]; int chg=0; for(int l=0;l<64;++l){sn[l]=l?E[l-1]:sc0; if(sn[l]!=S[l]) chg++;}
         if(!chg) break; rs_rounds++; rs_lanes_chg+=chg; int mxs=0,nl=0;
         uint32_t NE[64];
@@ -50,6 +65,7 @@ int main(int argc,char**argv){
       }
     }
   }}
+  printf("speculative entry (OV=%d): SIMT iterations %.2f/sc, lengths %.1f/sc\n", OV, (double)spec_iters/n_sc, (double)spec_lens/n_sc);
   printf("super-chunks %ld\nfirst walk: SIMT iterations %.2f, lengths/sc %.1f\nresync: rounds %.2f/sc, rounds needing lengths %.2f, SIMT len-iterations %.2f/sc, lanes changed %.1f/sc, lanes computing %.1f/sc, lengths %.1f/sc\n",
     n_sc,(double)walk_iters1/n_sc,(double)first_lens/n_sc,(double)rs_rounds/n_sc,(double)rs_rounds_needlen/n_sc,(double)rs_iters/n_sc,(double)rs_lanes_chg/n_sc,(double)rs_lenlanes/n_sc,(double)rs_lens/n_sc);
 }
