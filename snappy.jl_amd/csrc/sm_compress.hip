@@ -217,12 +217,11 @@ __device__ inline uint32_t writelane(uint32_t v, uint32_t l, uint32_t old) {
   return old;
 }
 
-// One block's parse by one wave.  kG: the table in global memory (u32 entries, tab = this wave's
-// 64 KiB slot; atomics in L2) instead of the LDS (u16 entries) -- the LDS then no longer caps the
-// parses per CU (diagnostic build SM_EXACT_GT, a design experiment).
-template <bool kG>
-__device__ __attribute__((always_inline)) inline void exact_block(const CompressArgs& a, const uint32_t b,
-                                                                  const uint32_t lane, uint32_t* stab) {
+__global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
+  __shared__ __attribute__((aligned(16))) uint32_t stab[kTabBytes / 4];
+
+  const uint32_t b = blockIdx.x;
+  const uint32_t lane = lane_id();
   const uint32_t n = a.in_len[b];
   uint8_t* dst = a.out + a.out_off[b];
   if (n > kBlockSize) {  // batch contract violated: refuse (positions are 16-bit)
@@ -234,11 +233,7 @@ __device__ __attribute__((always_inline)) inline void exact_block(const Compress
   S.nm4 = n - 4;
   const uint32_t tsize = a.table_size ? a.table_size : hashtable_size(n);      // Snappy.jl:27 (Q2)
   const uint32_t shift = 32 - (31 - __builtin_clz(tsize));                     // internal.jl:128
-  if constexpr (kG) {
-    for (uint32_t k = lane; k < tsize / 4; k += kWave) reinterpret_cast<uint4*>(stab)[k] = make_uint4(0, 0, 0, 0);
-  } else {
-    for (uint32_t k = lane; k < tsize / 2; k += kWave) stab[k] = 0;            // Snappy.jl:30
-  }
+  for (uint32_t k = lane; k < tsize / 2; k += kWave) stab[k] = 0;              // Snappy.jl:30
   // probe offsets D[64 i + lane] and D[64 i + lane + 1] (:170-172), in registers
   uint32_t Dk[kProbeSteps] = {}, Dn[kProbeSteps] = {};
   {
@@ -286,10 +281,7 @@ __device__ __attribute__((always_inline)) inline void exact_block(const Compress
         const uint32_t cur = S.word(p);
         h = hash32(cur, shift);
         raw = 0;
-        if (__builtin_expect(valid, 1)) {                                      // :190 (raw = candidate)
-          if constexpr (kG) raw = atomicExch(&stab[h], p);
-          else raw = tab_probe(stab, h, p);
-        }
+        if (__builtin_expect(valid, 1)) raw = tab_probe(stab, h, p);                                // :190 (raw = candidate)
         hm = ballot(valid && S.word(raw) == cur);                              // :193
         if (hm || ballot(valid) != ~0ull) break;                               // a match, or :175
       }
@@ -298,10 +290,8 @@ __device__ __attribute__((always_inline)) inline void exact_block(const Compress
       if (__builtin_expect(found, 1)) {
         const uint32_t j = ctz64(hm);
         const uint32_t pj = readlane(p, j);
-        if (valid && lane > j && raw <= pj) {                                  // undo later probes
-          if constexpr (kG) (void)atomicExch(&stab[h], raw);
-          else reinterpret_cast<uint16_t*>(stab)[h] = (uint16_t)raw;
-        }
+        if (valid && lane > j && raw <= pj)                                    // undo later probes
+          reinterpret_cast<uint16_t*>(stab)[h] = (uint16_t)raw;
         ip = pj;
         cand = readlane(raw, j);
       }
@@ -355,21 +345,11 @@ __device__ __attribute__((always_inline)) inline void exact_block(const Compress
           wc = uniform(S.word(ipn));
         }
         // (every lane stores the same value at the same address: one lane's store, no exec mask)
+        uint16_t* u = reinterpret_cast<uint16_t*>(stab);
+        u[hash32(wp, shift)] = (uint16_t)(ipn - 1);
         const uint32_t h2 = hash32(wc, shift);
-        uint32_t raw;
-        if constexpr (kG) {
-          uint32_t r0 = 0;
-          if (lane == 0) {
-            (void)atomicExch(&stab[hash32(wp, shift)], ipn - 1);
-            r0 = atomicExch(&stab[h2], ipn);
-          }
-          raw = readlane(r0, 0);
-        } else {
-          uint16_t* u = reinterpret_cast<uint16_t*>(stab);
-          u[hash32(wp, shift)] = (uint16_t)(ipn - 1);
-          raw = u[h2];
-          u[h2] = (uint16_t)ipn;
-        }
+        const uint32_t raw = u[h2];
+        u[h2] = (uint16_t)ipn;
         tk = writelane(ip | ((ip - cand) << 16), ntok, tk);
         tl = writelane(f, ntok, tl);
         ++ntok;
@@ -394,26 +374,6 @@ __device__ __attribute__((always_inline)) inline void exact_block(const Compress
   STAMP_FLUSH(g_stamp_x)
   if (lane == 0) a.out_len[b] = op;
 }
-
-__global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t stab[kTabBytes / 4];
-  exact_block<false>(a, blockIdx.x, lane_id(), stab);
-}
-
-#ifndef SM_EXACT_GT
-#define SM_EXACT_GT 0
-#endif
-#if SM_EXACT_GT
-constexpr uint32_t kExactSlotsPerCu = 16;
-// persistent: wave w parses blocks w, w + grid, ... with its own 64 KiB table slot
-__global__ __launch_bounds__(64) void k_compress_exact_g(CompressArgs a, uint32_t* gtab) {
-  uint32_t* const tab = gtab + (size_t)blockIdx.x * kMaxHashTableSize;
-  for (uint32_t b = blockIdx.x; b < a.nblk; b += gridDim.x) {
-    exact_block<true>(a, b, lane_id(), tab);
-    __threadfence_block();
-  }
-}
-#endif
 
 // ---- gather (single-stream assembly) ---------------------------------------------------
 
@@ -528,22 +488,6 @@ extern "C" int sm_debug_stamps_x(unsigned long long* out, int reset) {
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s) {
   if (a.nblk == 0) return hipSuccess;
   if (mode != 0) return launch_compress_fast(a, mode, s);
-#if SM_EXACT_GT
-  {
-    static uint32_t* gtab[64] = {};
-    static uint32_t nslot[64] = {};
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (!gtab[dev]) {
-      int ncu = 256;
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      nslot[dev] = (uint32_t)ncu * kExactSlotsPerCu;
-      if (hipMalloc(&gtab[dev], (size_t)nslot[dev] * kMaxHashTableSize * 4) != hipSuccess) return hipErrorOutOfMemory;
-    }
-    hipLaunchKernelGGL(k_compress_exact_g, dim3(min(a.nblk, nslot[dev])), dim3(64), 0, s, a, gtab[dev]);
-    return hipGetLastError();
-  }
-#endif
   hipLaunchKernelGGL(k_compress_exact, dim3(a.nblk), dim3(64), 0, s, a);
   return hipGetLastError();
 }

@@ -1374,9 +1374,11 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
   hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(64), 0, s, in, N, ip0, size, nchunks,
                      reinterpret_cast<const uint2*>(rec), deep, path, ctl, rounds);
   hipLaunchKernelGGL(k_origin_fill_dev, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
+  // (one pointer per thread: a pointer's hops are one dependent chain, so more threads hide more)
+  const uint32_t g1 = min(32768u, max(1u, (size + 255) / 256));
   for (uint32_t r = 0; r < rounds; ++r)
-    hipLaunchKernelGGL(k_origin_resolve_hops, dim3(origin_grid(size)), dim3(256), 0, s, P, size, ctl + 4, r);
-  hipLaunchKernelGGL(k_origin_gather, dim3(origin_grid(size)), dim3(256), 0, s, in, P, size, out);
+    hipLaunchKernelGGL(k_origin_resolve_hops, dim3(g1), dim3(256), 0, s, P, size, ctl + 4, r);
+  hipLaunchKernelGGL(k_origin_gather, dim3(g1), dim3(256), 0, s, in, P, size, out);
   return hipGetLastError();
 }
 
