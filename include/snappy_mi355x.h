@@ -189,8 +189,9 @@ sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, siz
  * (Ptr{UInt8}, Csize_t, Ptr{UInt8}, Ref{Csize_t}) -> Cint), so a Julia binding switches from
  * libsnappy by library and symbol name alone.  The default context is created on first use on
  * device $SNAPPY_MI355X_DEVICE (default 0); calls are serialised on it.
- * sm_snappy_compress uses SM_MODE_FAST unless sm_snappy_set_mode() selects another mode
- * (SM_MODE_REFERENCE for Snappy.jl's exact bytes). */
+ * sm_snappy_compress uses SM_MODE_FAST_DENSE (sizes within 1.01x of Snappy.jl's) unless
+ * sm_snappy_set_mode() selects another mode (SM_MODE_REFERENCE for Snappy.jl's exact bytes,
+ * SM_MODE_FAST for the highest rate). */
 sm_status sm_snappy_compress(const char* input, size_t input_length, char* compressed, size_t* compressed_length);
 sm_status sm_snappy_uncompress(const char* compressed, size_t compressed_length, char* uncompressed,
                                size_t* uncompressed_length);

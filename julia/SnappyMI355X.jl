@@ -89,7 +89,7 @@ end
 
 # test/libsnappy.jl:5-30's ccall signatures, rebound by library and symbol name alone: the
 # ctx-less snappy-c.h-shaped entry points (a default context on device $SNAPPY_MI355X_DEVICE,
-# SM_MODE_FAST unless sm_snappy_set_mode says otherwise).
+# SM_MODE_FAST_DENSE unless sm_snappy_set_mode says otherwise).
 function gpu_compress(src::Vector{UInt8})
     cap = ccall((:sm_snappy_max_compressed_length, LIB), Csize_t, (Csize_t,), length(src))
     dst = newbytes(cap)

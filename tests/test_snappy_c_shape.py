@@ -90,9 +90,13 @@ def test_host_only_entry_points(sm):
 @pytest.mark.gpu
 def test_ccall_shape_roundtrip(sm, oracle, gpu_available):
     L = _bind(ctypes.CDLL(sm.library_path()))
+    # the default mode is dense: the same bytes as the ctx API's SM_MODE_FAST_DENSE
+    raw = read_testfile("alice29.txt")
+    st, comp = ccall_compress(L, raw)
+    assert st == 0 and comp == sm.compress(raw, mode="dense") and oracle.uncompress(comp) == raw
     for fname in ("html", "alice29.txt", "fireworks.jpeg", "urls.10K"):
         raw = read_testfile(fname)
-        assert L.sm_snappy_set_mode(1) == 0  # SM_MODE_FAST, the default
+        assert L.sm_snappy_set_mode(1) == 0  # SM_MODE_FAST
         st, comp = ccall_compress(L, raw)
         assert st == 0 and oracle.uncompress(comp) == raw
         st, back = ccall_uncompress(L, comp)
@@ -100,6 +104,6 @@ def test_ccall_shape_roundtrip(sm, oracle, gpu_available):
         assert L.sm_snappy_set_mode(0) == 0  # SM_MODE_REFERENCE: Snappy.jl's exact bytes
         st, comp = ccall_compress(L, raw)
         assert st == 0 and comp == oracle.compress(raw)
-    L.sm_snappy_set_mode(1)
+    L.sm_snappy_set_mode(2)  # back to the default
     st, _ = ccall_uncompress(L, read_testfile("baddata1.snappy"))
     assert st != 0
