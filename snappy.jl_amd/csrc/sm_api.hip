@@ -44,9 +44,13 @@ struct DevBuf {
 
 // Host staging: page-aligned ordinary memory registered for DMA (hipHostRegister), so the CPU
 // reads it through its caches -- the host walks the index records and scatters batch outputs
-// from it.  (hipHostMalloc'd staging was read ~2x slower by those CPU loops.)
+// from it.  (hipHostMalloc'd staging was read ~2x slower by those CPU loops.)  It is also mapped
+// into the device (dp): the single-buffer calls' last kernel writes its result there directly,
+// because a copy-engine transfer queued behind kernels waited up to ~120 us on this box
+// (tools/probes/latency_probe.hip, profiles/r04_latency_probe.txt).
 struct HostBuf {
   void* p = nullptr;
+  void* dp = nullptr;  // the device's address of p (nullptr: not mapped)
   size_t cap = 0;
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
@@ -54,13 +58,14 @@ struct HostBuf {
     const size_t want = ((n < (1u << 20) ? (1u << 20) : n) + 4095) & ~(size_t)4095;
     void* q = nullptr;
     if (posix_memalign(&q, 4096, want) != 0) return hipErrorOutOfMemory;
-    const hipError_t e = hipHostRegister(q, want, hipHostRegisterDefault);
+    const hipError_t e = hipHostRegister(q, want, hipHostRegisterMapped);
     if (e != hipSuccess) {
       free(q);
       return e;
     }
     p = q;
     cap = want;
+    if (hipHostGetDevicePointer(&dp, q, 0) != hipSuccess) dp = nullptr;
     return hipSuccess;
   }
   void release() {
@@ -69,6 +74,7 @@ struct HostBuf {
       free(p);
     }
     p = nullptr;
+    dp = nullptr;
     cap = 0;
   }
 };
@@ -363,6 +369,7 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
 constexpr uint32_t kSmallMinOutput = SM_SMALL_MIN;  // smaller streams: the one-wave decode
 constexpr uint32_t kSmallMaxChunks = 1024;         // compressed bodies up to 1 MiB
 constexpr uint32_t kSmallMaxOutput = 64u << 20;    // 4 B of origin pointer per output byte
+constexpr uint32_t kPinnedOutMax = 16u << 20;      // outputs the last kernel writes into the pinned staging
 
 int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8_t* host_out) {
   using sm::kIdxEntries;
@@ -375,18 +382,24 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   const size_t ctl_n = 4 + rounds;
   if (ctx->idx.ensure(ctl_off + ctl_n * 4) != hipSuccess) return 0;
   if (ctx->org.ensure((size_t)size * 4) != hipSuccess) return 0;
+  // the output and the verdict words straight into the pinned staging (a large output: the words
+  // only, the output by a copy into host_out)
+  const bool pin_out = size <= kPinnedOutMax;
+  const size_t w_off = pin_out ? align_up(size, 256) : 0;
+  if (ctx->stage.ensure(w_off + 64) != hipSuccess || !ctx->stage.dp) return 0;
   hipStream_t s = ctx->stream;
   uint8_t* ib = (uint8_t*)ctx->idx.p;
   uint32_t* d_ctl = (uint32_t*)(ib + ctl_off);
+  uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
   if (sm::launch_small_decode((const uint8_t*)ctx->in.p, n, ip0, size, nchunks, (uint32_t*)ib,
                               (sm::OriginPath*)(ib + path_off), d_ctl, (uint32_t*)ctx->org.p, rounds,
-                              (uint8_t*)ctx->out.p, s) != hipSuccess)
+                              pin_out ? sdp : (uint8_t*)ctx->out.p, (uint32_t*)(sdp + w_off), s) != hipSuccess)
     return -1;
-  uint32_t ctl[4 + 32];
-  if (hipMemcpyAsync(ctl, d_ctl, ctl_n * 4, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
-  if (hipMemcpyAsync(host_out, ctx->out.p, size, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
+  if (!pin_out && hipMemcpyAsync(host_out, ctx->out.p, size, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
-  if (ctl[1] || ctl[2] || ctl[4 + rounds - 1]) return 0;  // (the last: never, by the round count)
+  const volatile uint32_t* w = (const volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off);
+  if (w[0] || w[1] || w[2]) return 0;  // (the last: never, by the round count)
+  if (pin_out) memcpy(host_out, ctx->stage.p, size);
   return 4;
 }
 
@@ -871,26 +884,27 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   uint32_t* d_out_len = (uint32_t*)(m + 28 * (size_t)nfrag);
   HT_DECL
   // Small inputs: one synchronisation -- the fragment table and the gather (with the lengths'
-  // prefix sums) on the device, the stream body down into the context's pinned staging (its capacity bound, not
-  // its length, which only the device knows), then copied out on the host.
-  if (n <= kSmallCompressMax && ctx->stage.ensure(sm_max_compressed_length(n) + 16) == hipSuccess) {
-    uint64_t* d_tot = (uint64_t*)(m + 32 * (size_t)nfrag);
+  // prefix sums) on the device; the gather kernel writes the stream body into the context's
+  // pinned staging (device-mapped: no copy engine behind the kernels), copied out on the host.
+  const size_t t_off = align_up(sm_max_compressed_length(n) + 16, 256);
+  if (n <= kSmallCompressMax && ctx->stage.ensure(t_off + 16) == hipSuccess && ctx->stage.dp) {
     SM_CHECK(hipMemcpyAsync(ctx->in.p, input, n, hipMemcpyHostToDevice, s));
     SM_CHECK(sm::launch_frag_plan(n, nfrag, slot, d_in_off, d_in_len, d_out_off, s));
     sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
                        nfrag, sm::hashtable_size(n), 0};
     SM_CHECK(sm::launch_compress(a, mode, s));
-    SM_CHECK(sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag, d_tot,
-                                    (uint8_t*)ctx->out2.p, s));
-    uint64_t tot[2] = {0, 0};
-    SM_CHECK(hipMemcpyAsync(tot, d_tot, 16, hipMemcpyDeviceToHost, s));
-    SM_CHECK(hipMemcpyAsync(ctx->stage.p, ctx->out2.p, sm_max_compressed_length(n) - hl, hipMemcpyDeviceToHost, s));
+    // the gather writes the body and its (length, error) pair straight into the pinned staging
+    uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
+    SM_CHECK(sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag,
+                                    (uint64_t*)(sdp + t_off), sdp, s));
     SM_CHECK(hipStreamSynchronize(s));
     HT("compress (small): all")
+    const volatile uint64_t* tot = (const volatile uint64_t*)((uint8_t*)ctx->stage.p + t_off);
+    const uint64_t len = tot[0];
     if (tot[1]) return SM_ERR_DEVICE;  // a block's error mark (SM_OUT_LEN_ERROR), never expected
-    if (hl + tot[0] > *compressed_length) return SM_BUFFER_TOO_SMALL;
-    memcpy(compressed + hl, ctx->stage.p, tot[0]);
-    *compressed_length = hl + tot[0];
+    if (hl + len > *compressed_length) return SM_BUFFER_TOO_SMALL;
+    memcpy(compressed + hl, ctx->stage.p, len);
+    *compressed_length = hl + len;
     return SM_OK;
   }
   SM_CHECK(hipMemcpyAsync(d_in_off, in_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
@@ -963,7 +977,6 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   uint32_t* d_out_len = (uint32_t*)(m + 16);
   int32_t* d_status = (int32_t*)(m + 20);
   uint32_t hv[2] = {(uint32_t)n, size};
-  uint64_t zero = 0;
   HT_DECL
   SM_CHECK(hipMemcpyAsync(ctx->in.p, compressed, n, hipMemcpyHostToDevice, s));
   HT("uncompress: H2D input")
@@ -1006,11 +1019,26 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
     }
   }
   ctx->last_path = 0;
-  SM_CHECK(hipMemcpyAsync(d_off, &zero, 8, hipMemcpyHostToDevice, s));
-  SM_CHECK(hipMemcpyAsync(d_in_len, hv, 8, hipMemcpyHostToDevice, s));
+  const uint32_t hm[4] = {0, 0, hv[0], hv[1]};  // d_off (u64 0), d_in_len, d_cap
+  SM_CHECK(hipMemcpyAsync(d_off, hm, 16, hipMemcpyHostToDevice, s));
   sm::DecompressArgs a{(const uint8_t*)ctx->in.p, d_off, d_in_len, (uint8_t*)ctx->out.p, d_off, d_cap, d_out_len,
                        d_status, 1};
   SM_CHECK(sm::launch_decompress(a, size > SM_BLOCK_SIZE, s));
+  // the output (whatever the status) and (out_len, status) into the pinned staging by a kernel
+  const size_t w_off = align_up(size, 256);
+  if (size <= kPinnedOutMax && ctx->stage.ensure(w_off + 64) == hipSuccess && ctx->stage.dp) {
+    uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
+    SM_CHECK(sm::launch_to_host((const uint8_t*)ctx->out.p, size, sdp, d_out_len, 2, (uint32_t*)(sdp + w_off), s));
+    SM_CHECK(hipStreamSynchronize(s));
+    const volatile uint32_t* w = (const volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off);
+    const uint32_t dlen = w[0];
+    const int32_t dst = (int32_t)w[1];
+    if (dst != SM_OK) return dst;
+    if (dlen > size) return SM_ERR_DEVICE;  // (never: the kernel's bound)
+    memcpy(uncompressed, ctx->stage.p, dlen);
+    *uncompressed_length = dlen;
+    return SM_OK;
+  }
   int32_t dst = 0;
   uint32_t dlen = 0;
   SM_CHECK(hipMemcpyAsync(&dst, d_status, 4, hipMemcpyDeviceToHost, s));

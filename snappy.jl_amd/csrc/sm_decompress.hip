@@ -1308,8 +1308,15 @@ __global__ __launch_bounds__(64) void k_origin_fill_dev(const uint8_t* __restric
 // Pointer jumping with up to kHops chain steps per pointer per launch: after launch r every
 // unresolved pointer has moved >= kHops^(r+1) steps.  Launch r > 0 returns at once when launch
 // r - 1 left nothing pending (pend[r] counts waves with unresolved pointers after launch r).
+// Nothing runs when the chain or a fill failed (ctl[1], ctl[2]): P is then not all written.
 constexpr uint32_t kHops = kSmallHops;
-__global__ __launch_bounds__(256) void k_origin_resolve_hops(uint32_t* P, uint32_t size, uint32_t* pend, uint32_t r) {
+__device__ inline bool small_failed(const uint32_t* ctl) {
+  return (__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+          __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
+}
+__global__ __launch_bounds__(256) void k_origin_resolve_hops(uint32_t* P, uint32_t size, uint32_t* ctl, uint32_t r) {
+  uint32_t* const pend = ctl + 4;
+  if (small_failed(ctl)) return;
   if (r > 0 && __hip_atomic_load(&pend[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   uint32_t left = 0;
   for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < size; x += gridDim.x * blockDim.x) {
@@ -1342,6 +1349,51 @@ __global__ __launch_bounds__(256) void k_origin_gather(const uint8_t* __restrict
     out[x] = in[P[x] & 0x7fffffffu];
 }
 
+// Path 4's last launch: thread 0 publishes the call's verdict words (ctl[1], ctl[2], the last
+// round's pending count) to `words`, then -- unless the chain or a fill failed -- out[x] =
+// in[P[x] & 0x7fffffff], four bytes a thread (one 16-byte P load, one u32 store).  out and words may
+// be the caller's pinned host memory (device-mapped): the result then goes straight over PCIe,
+// with no copy engine behind the kernels.
+__global__ __launch_bounds__(256) void k_small_gather(const uint8_t* __restrict__ in, const uint32_t* __restrict__ P,
+                                                      uint32_t size, uint8_t* __restrict__ out, const uint32_t* ctl,
+                                                      uint32_t rounds, uint32_t* words) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) {
+    words[0] = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    words[1] = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    words[2] = __hip_atomic_load(&ctl[4 + rounds - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (small_failed(ctl)) return;
+  const uint32_t nw = size / 4;
+  for (uint32_t w = t; w < nw; w += gridDim.x * blockDim.x) {
+    const uint4 q = reinterpret_cast<const uint4*>(P)[w];
+    const uint32_t v = (uint32_t)in[q.x & 0x7fffffffu] | ((uint32_t)in[q.y & 0x7fffffffu] << 8) |
+                       ((uint32_t)in[q.z & 0x7fffffffu] << 16) | ((uint32_t)in[q.w & 0x7fffffffu] << 24);
+    reinterpret_cast<uint32_t*>(out)[w] = v;
+  }
+  if (t < size - 4 * nw) out[4 * nw + t] = in[P[4 * nw + t] & 0x7fffffffu];
+}
+
+// src[0, n) -> dst and nw control words -> words (dst / words: pinned host memory, device-mapped),
+// 16 bytes a thread; src and dst 16-byte aligned.
+__global__ __launch_bounds__(256) void k_to_host(const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ dst,
+                                                 const uint32_t* wsrc, uint32_t nw, uint32_t* words) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nw) words[t] = wsrc[t];
+  const uint32_t n16 = n / 16;
+  for (uint32_t i = t; i < n16; i += gridDim.x * blockDim.x)
+    reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
+  if (t < n - 16 * n16) dst[16 * n16 + t] = src[16 * n16 + t];
+}
+
+hipError_t launch_to_host(const uint8_t* src, uint32_t n, uint8_t* dst, const uint32_t* wsrc, uint32_t nw,
+                          uint32_t* words, hipStream_t s) {
+  if (nw > 256) return hipErrorInvalidValue;
+  const uint32_t grid = min(1024u, max(1u, (n / 16 + 255) / 256));
+  hipLaunchKernelGGL(k_to_host, dim3(grid), dim3(256), 0, s, src, n, dst, wsrc, nw, words);
+  return hipGetLastError();
+}
+
 hipError_t launch_origin_fill(const uint8_t* in, uint32_t N, uint32_t size, const OriginPath* path, uint32_t npath,
                               uint32_t* P, int32_t* status, hipStream_t s) {
   if (npath == 0) return hipSuccess;
@@ -1366,7 +1418,7 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
 
 hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
                                uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
-                               uint8_t* out, hipStream_t s) {
+                               uint8_t* out, uint32_t* words, hipStream_t s) {
   if (nchunks == 0 || size == 0 || rounds == 0 || 4 + rounds > kWave) return hipErrorInvalidValue;
   uint4* deep = reinterpret_cast<uint4*>(rec + (size_t)nchunks * kIdxEntries * 2);  // kDeepLevels per chunk
   hipLaunchKernelGGL((k_stream_index<kSmallChunk, true>), dim3(nchunks), dim3(64), 0, s, in, N, ip0,
@@ -1377,8 +1429,9 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
   // (one pointer per thread: a pointer's hops are one dependent chain, so more threads hide more)
   const uint32_t g1 = min(32768u, max(1u, (size + 255) / 256));
   for (uint32_t r = 0; r < rounds; ++r)
-    hipLaunchKernelGGL(k_origin_resolve_hops, dim3(g1), dim3(256), 0, s, P, size, ctl + 4, r);
-  hipLaunchKernelGGL(k_origin_gather, dim3(g1), dim3(256), 0, s, in, P, size, out);
+    hipLaunchKernelGGL(k_origin_resolve_hops, dim3(g1), dim3(256), 0, s, P, size, ctl, r);
+  const uint32_t g4 = min(8192u, max(1u, (size / 4 + 255) / 256));
+  hipLaunchKernelGGL(k_small_gather, dim3(g4), dim3(256), 0, s, in, P, size, out, ctl, rounds, words);
   return hipGetLastError();
 }
 

@@ -81,10 +81,16 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
 // 16-byte deep-entry records; path: nchunks elements; ctl: 4 +
 // rounds u32 (zeroed by the chain kernel) -- ctl[0] path elements, ctl[1] != 0: the chain found no exact path (fall
 // back), ctl[2] != 0: an element failed its checks (fall back), ctl[4 + r] != 0: pointers still
-// unresolved after round r.  P: size u32.
+// unresolved after round r.  P: size u32.  The last launch writes words[0..2] = ctl[1], ctl[2],
+// ctl[4 + rounds - 1] (the call's verdict) and the output; out and words may be device-mapped
+// pinned host memory.
 hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
                                uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
-                               uint8_t* out, hipStream_t s);
+                               uint8_t* out, uint32_t* words, hipStream_t s);
+// src[0, n) to dst and wsrc[0, nw) to words by a kernel (dst, words: device-mapped pinned host
+// memory; no copy engine behind the kernels).  src, dst 16-byte aligned; nw <= 256.
+hipError_t launch_to_host(const uint8_t* src, uint32_t n, uint8_t* dst, const uint32_t* wsrc, uint32_t nw,
+                          uint32_t* words, hipStream_t s);
 hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s);
 // sm_compress, small inputs (at most 64 fragments), without host round trips: the fragments'
 // offsets and lengths (fragment f = input [64 KiB f, +64 KiB), output slot f at pitch `slot`);

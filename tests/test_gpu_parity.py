@@ -702,3 +702,29 @@ def test_host_path_piece_boundaries(sm, oracle, gpu_available):
             ref = sm.compress(raw, mode="reference")
             assert ref == oracle.compress(raw)
             assert sm.uncompress(ref) == raw
+
+
+def test_single_calls_through_pinned_staging(sm, oracle, gpu_available):
+    """The single-buffer calls' last kernel writes its result into the context's device-mapped
+    pinned staging (sm_api.hip HostBuf::dp): back-to-back calls of equal sizes and different
+    contents, alternating paths 0 and 4 and compress modes, never see a previous call's bytes or
+    verdict words.  Includes a failing path-4 call (mutated stream: the fallback decides) between
+    good ones, and output sizes not a multiple of 4 or 16."""
+    rng = np.random.default_rng(0x57A6E)
+    text = read_testfile("alice29.txt")
+    for size in (4096 + 3, 65536 + 13, 150001):
+        a = text[:size]
+        b = bytes(reversed(text[:size]))
+        lit = rng.integers(0, 256, size, dtype=np.uint8).tobytes()  # path 0 (mostly literals)
+        streams = [(x, sm.compress(x, mode=m)) for x in (a, b, lit) for m in ("fast", "dense", "reference")]
+        for x, c in streams:
+            assert oracle.uncompress(c) == x
+        for rep in range(3):
+            for x, c in streams:
+                assert sm.compress(x, mode="reference") == oracle.compress(x)
+                assert sm.uncompress(c) == x
+            x, c = streams[rep]
+            bad = bytearray(c)
+            bad[len(bad) // 2] ^= 0x5C
+            bad = bytes(bad)
+            assert _status(sm, bad) == oracle.uncompress_status(bad)

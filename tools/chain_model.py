@@ -1,0 +1,113 @@
+"""CPU model of path 4's device chain (k_stream_chain, sm_decompress.hip) on a stream: how many
+path elements the chain takes from the index's entry records, from the deep records, or by its own
+serial walk (dev_walk, the slow case).  Design tool:  python3 tools/chain_model.py STREAM... [--levels K]
+Streams from tools/dump_streams.py (gpurun_out/streams/)."""
+import argparse
+
+KC = 1024        # kSmallChunk
+ENTRIES = 64     # kIdxEntries
+
+
+def varint(b):
+    v, s, i = 0, 0, 0
+    while True:
+        x = b[i]
+        v |= (x & 0x7F) << s
+        i += 1
+        if x < 0x80:
+            return v, i
+        s += 7
+
+
+def tag(b, p):
+    """(size in the stream, output bytes) of the tag at p, bytes past the end read as zero."""
+    def at(i):
+        return b[i] if i < len(b) else 0
+    c = at(p)
+    t = c & 3
+    if t == 0:
+        n = c >> 2
+        if n < 60:
+            return 1 + n + 1, n + 1
+        tl = n - 59
+        tr = 0
+        for j in range(tl):
+            tr |= at(p + 1 + j) << (8 * j)
+        return 1 + tl + tr + 1, tr + 1
+    if t == 1:
+        return 2, ((c >> 2) & 7) + 4
+    if t == 2:
+        return 3, (c >> 2) + 1
+    return 5, (c >> 2) + 1
+
+
+def walk(b, p, lim):
+    o = 0
+    while p < lim:
+        s, ob = tag(b, p)
+        p += s
+        o += ob
+    return p, o
+
+
+def model(b, levels):
+    N = len(b)
+    size, ip0 = varint(b)
+    nch = (N - ip0 + KC - 1) // KC
+    deep = []
+    for c in range(nch):
+        s = ip0 + c * KC
+        x, _ = walk(b, s, min(s + KC, N - 1))
+        lv = []
+        for _ in range(levels):
+            dl = (x - ip0) // KC
+            db = ip0 + dl * KC
+            if not (x < N - 1 and x - db >= ENTRIES):
+                break
+            dex, _ = walk(b, x, min(db + KC, N - 1))
+            lv.append((x, dex))
+            x = dex
+        deep.append(lv)
+    y, n_rec, n_deep, n_walk = ip0, 0, 0, 0
+    cprev, dsrc, dlev = None, None, 0
+    walk_bytes = 0
+    while y < N - 1:
+        c = (y - ip0) // KC
+        base = ip0 + c * KC
+        l = y - base
+        if l < ENTRIES:
+            ex, _ = walk(b, y, min(base + KC, N - 1))
+            n_rec += 1
+            dsrc = None
+        else:
+            hit = None
+            if dsrc is not None and dlev + 1 < len(deep[dsrc]) and deep[dsrc][dlev + 1][0] == y:
+                hit = (dsrc, dlev + 1)
+            elif cprev is not None and deep[cprev] and deep[cprev][0][0] == y:
+                hit = (cprev, 0)
+            ex, _ = walk(b, y, min(base + KC, N - 1))
+            if hit:
+                n_deep += 1
+                dsrc, dlev = hit
+            else:
+                n_walk += 1
+                walk_bytes += min(base + KC, N - 1) - y
+                dsrc = None
+        cprev = c
+        y = ex
+    return nch, n_rec, n_deep, n_walk, walk_bytes
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("streams", nargs="+")
+    ap.add_argument("--levels", type=int, default=4)
+    a = ap.parse_args()
+    print("%-40s %6s %6s %6s %6s %8s" % ("stream", "chunks", "rec", "deep", "walks", "walk B"))
+    for f in a.streams:
+        b = open(f, "rb").read()
+        print("%-40s %6d %6d %6d %6d %8d" % ((f.split("/")[-1],) + model(b, a.levels)))
+
+
+if __name__ == "__main__":
+    main()
