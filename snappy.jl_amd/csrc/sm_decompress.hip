@@ -1306,26 +1306,45 @@ __global__ __launch_bounds__(64) void k_origin_fill_dev(const uint8_t* __restric
 }
 
 // Pointer jumping with up to kHops chain steps per pointer per launch: after launch r every
-// unresolved pointer has moved >= kHops^(r+1) steps.  Launch r > 0 returns at once when launch
-// r - 1 left nothing pending (pend[r] counts waves with unresolved pointers after launch r).
-// Nothing runs when the chain or a fill failed (ctl[1], ctl[2]): P is then not all written.
+// unresolved pointer has moved >= kHops^(r+1) steps, so ceil(log_kHops(size)) launches resolve
+// all.  One pointer per thread (a pointer's hops are one dependent chain, so more threads hide
+// more); a byte is written to out in the launch in which its pointer resolves (the gather folded
+// in: a pointer resolved at the start of launch r > 0 was written before).  Launch r > 0 returns
+// at once when launch r - 1 left nothing pending (pend[r] counts waves with unresolved pointers
+// after launch r).  Launch 0's first thread publishes
+// the call's verdict words (ctl[1], ctl[2]); nothing else runs when the chain or a fill failed (P
+// is then not all written).  out and words may be device-mapped pinned host memory.
 constexpr uint32_t kHops = kSmallHops;
 __device__ inline bool small_failed(const uint32_t* ctl) {
   return (__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
           __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
 }
-__global__ __launch_bounds__(256) void k_origin_resolve_hops(uint32_t* P, uint32_t size, uint32_t* ctl, uint32_t r) {
+__global__ __launch_bounds__(256) void k_small_resolve(const uint8_t* __restrict__ in, uint32_t* P, uint32_t size,
+                                                       uint32_t* ctl, uint32_t r, uint8_t* __restrict__ out,
+                                                       uint32_t* words) {
   uint32_t* const pend = ctl + 4;
+  const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r == 0 && t0 == 0) {
+    words[0] = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    words[1] = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    words[2] = 0;
+  }
   if (small_failed(ctl)) return;
   if (r > 0 && __hip_atomic_load(&pend[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
   uint32_t left = 0;
-  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < size; x += gridDim.x * blockDim.x) {
+  for (uint32_t x = t0; x < size; x += gridDim.x * blockDim.x) {
     uint32_t v = P[x];
-    if (v >> 31) continue;
+    if (v >> 31) {
+      if (r == 0) out[x] = in[v & 0x7fffffffu];  // (r > 0: written by an earlier launch)
+      continue;
+    }
 #pragma unroll 1
     for (uint32_t h = 0; h < kHops && !(v >> 31); ++h) v = P[v];  // v < x: an earlier byte of the chain
     P[x] = v;
-    left += !(v >> 31);
+    if (v >> 31)
+      out[x] = in[v & 0x7fffffffu];
+    else
+      ++left;
   }
   if (__builtin_amdgcn_ballot_w64(left != 0) && lane_id() == 0) atomicAdd(&pend[r], 1u);
 }
@@ -1347,31 +1366,6 @@ __global__ __launch_bounds__(256) void k_origin_gather(const uint8_t* __restrict
                                                        uint32_t size, uint8_t* __restrict__ out) {
   for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < size; x += gridDim.x * blockDim.x)
     out[x] = in[P[x] & 0x7fffffffu];
-}
-
-// Path 4's last launch: thread 0 publishes the call's verdict words (ctl[1], ctl[2], the last
-// round's pending count) to `words`, then -- unless the chain or a fill failed -- out[x] =
-// in[P[x] & 0x7fffffff], four bytes a thread (one 16-byte P load, one u32 store).  out and words may
-// be the caller's pinned host memory (device-mapped): the result then goes straight over PCIe,
-// with no copy engine behind the kernels.
-__global__ __launch_bounds__(256) void k_small_gather(const uint8_t* __restrict__ in, const uint32_t* __restrict__ P,
-                                                      uint32_t size, uint8_t* __restrict__ out, const uint32_t* ctl,
-                                                      uint32_t rounds, uint32_t* words) {
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t == 0) {
-    words[0] = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    words[1] = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    words[2] = __hip_atomic_load(&ctl[4 + rounds - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (small_failed(ctl)) return;
-  const uint32_t nw = size / 4;
-  for (uint32_t w = t; w < nw; w += gridDim.x * blockDim.x) {
-    const uint4 q = reinterpret_cast<const uint4*>(P)[w];
-    const uint32_t v = (uint32_t)in[q.x & 0x7fffffffu] | ((uint32_t)in[q.y & 0x7fffffffu] << 8) |
-                       ((uint32_t)in[q.z & 0x7fffffffu] << 16) | ((uint32_t)in[q.w & 0x7fffffffu] << 24);
-    reinterpret_cast<uint32_t*>(out)[w] = v;
-  }
-  if (t < size - 4 * nw) out[4 * nw + t] = in[P[4 * nw + t] & 0x7fffffffu];
 }
 
 // src[0, n) -> dst and nw control words -> words (dst / words: pinned host memory, device-mapped),
@@ -1426,12 +1420,9 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
   hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(64), 0, s, in, N, ip0, size, nchunks,
                      reinterpret_cast<const uint2*>(rec), deep, path, ctl, rounds);
   hipLaunchKernelGGL(k_origin_fill_dev, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
-  // (one pointer per thread: a pointer's hops are one dependent chain, so more threads hide more)
   const uint32_t g1 = min(32768u, max(1u, (size + 255) / 256));
   for (uint32_t r = 0; r < rounds; ++r)
-    hipLaunchKernelGGL(k_origin_resolve_hops, dim3(g1), dim3(256), 0, s, P, size, ctl, r);
-  const uint32_t g4 = min(8192u, max(1u, (size / 4 + 255) / 256));
-  hipLaunchKernelGGL(k_small_gather, dim3(g4), dim3(256), 0, s, in, P, size, out, ctl, rounds, words);
+    hipLaunchKernelGGL(k_small_resolve, dim3(g1), dim3(256), 0, s, in, P, size, ctl, r, out, words);
   return hipGetLastError();
 }
 
