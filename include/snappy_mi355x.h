@@ -91,6 +91,12 @@ int sm_ctx_last_path(sm_ctx* ctx);
 /* diagnostic: enable (1, the default) or disable (0) path 4 for the ctx's sm_uncompress calls
  * (the tests run the other paths on small streams with it off) */
 sm_status sm_ctx_set_small_decode(sm_ctx* ctx, int enable);
+/* diagnostic: enable (1, the default) or disable (0) parsing the fragments of a small fast-mode
+ * sm_compress input (<= 4 MiB) in parts on their own workgroups -- the same bytes as the
+ * whole-fragment parse, at a fraction of its latency; sm_ctx_last_compress_split: 1 when the
+ * ctx's last sm_compress did so, 0 when not, -1 for a null ctx */
+sm_status sm_ctx_set_split_compress(sm_ctx* ctx, int enable);
+int sm_ctx_last_compress_split(sm_ctx* ctx);
 
 /* ---- single buffer, host memory (the reference's exported API) -------------------- */
 /* replaces compress(::Vector{UInt8}), src/Snappy.jl:20-36 (and compress(::String), :38).

@@ -44,6 +44,7 @@ ABI_SYMBOLS = (
     "sm_encode32", "sm_ctx_create", "sm_ctx_destroy", "sm_ctx_stream", "sm_compress", "sm_uncompress",
     "sm_compress_batch_device", "sm_uncompress_batch_device", "sm_compress_batch",
     "sm_uncompress_batch", "sm_version", "sm_compress_fragments_device", "sm_ctx_last_path", "sm_ctx_set_small_decode",
+    "sm_ctx_set_split_compress", "sm_ctx_last_compress_split",
     "sm_find_match_length", "sm_validate_batch_device", "sm_uncompressed_length_batch_device",
     "sm_validate_compressed_buffer", "sm_compress_batch_sharded", "sm_uncompress_batch_sharded",
     "sm_uncompress_fragments_device", "sm_snappy_compress", "sm_snappy_uncompress",
@@ -122,6 +123,10 @@ def load_library(path):
     L.sm_ctx_last_path.argtypes = [vp]
     L.sm_ctx_set_small_decode.restype = ctypes.c_int
     L.sm_ctx_set_small_decode.argtypes = [vp, ctypes.c_int]
+    L.sm_ctx_set_split_compress.restype = ctypes.c_int
+    L.sm_ctx_set_split_compress.argtypes = [vp, ctypes.c_int]
+    L.sm_ctx_last_compress_split.restype = ctypes.c_int
+    L.sm_ctx_last_compress_split.argtypes = [vp]
     L.sm_version.restype = ctypes.c_char_p
     L.sm_version.argtypes = []
     L.sm_compress_fragments_device.restype = i32
@@ -269,6 +274,19 @@ def set_small_decode(enable, device=0):
     st = lib().sm_ctx_set_small_decode(context(device), 1 if enable else 0)
     if st:
         raise SnappyError(st)
+
+
+def set_split_compress(enable, device=0):
+    """Diagnostic: compress() of small fast-mode inputs parses each 64 KiB fragment in parts on
+    their own workgroups (on by default; the same bytes either way)."""
+    st = lib().sm_ctx_set_split_compress(context(device), 1 if enable else 0)
+    if st:
+        raise SnappyError(st)
+
+
+def last_compress_split(device=0):
+    """Whether the last compress() on this device parsed its fragments in parts."""
+    return int(lib().sm_ctx_last_compress_split(context(device))) == 1
 
 
 def uncompress(data, device=0):

@@ -399,6 +399,42 @@ __global__ __launch_bounds__(256) void k_frag_plan(uint64_t n, uint32_t nfrag, u
   out_off[f] = (uint64_t)f * slot;
 }
 
+// n bytes from s8 (16-byte aligned) to g (any alignment) by the workgroup's part y of ny:
+// aligned 16-byte stores of byte-shifted units, the partial units at both ends by bytes (part 0;
+// they share a 16-byte unit with the neighbouring pieces)
+__device__ __attribute__((always_inline)) inline void gather_unit(const uint8_t* __restrict__ s8, uint32_t n,
+                                                                 uint8_t* __restrict__ g, uint32_t y, uint32_t ny) {
+  const uint4* s16 = reinterpret_cast<const uint4*>(s8);
+  const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
+  const uint32_t u0 = ad ? 1u : 0u, u1 = (n + ad) >> 4;  // whole units [u0, u1); unit u = bytes [16u - ad, +16)
+  uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
+  const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;
+  const uint32_t stride = blockDim.x * ny;
+  for (uint32_t u = u0 + y * blockDim.x + threadIdx.x; u < u1; u += stride) {
+    const uint32_t j = 16 * u - ad;
+    const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
+    const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+    uint32_t r5[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      uint32_t vv = x[q];
+#pragma unroll
+      for (int dd = 1; dd < 4; ++dd) vv = dw == (uint32_t)dd ? x[q + dd] : vv;
+      r5[q] = vv;
+    }
+    g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
+                        __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
+  }
+  if (y == 0) {
+    const uint32_t nh = min(u0 ? 16 - ad : 0u, n);
+    const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);
+    if (threadIdx.x < nh + (n - tb)) {
+      const uint32_t jj = threadIdx.x < nh ? threadIdx.x : tb + (threadIdx.x - nh);
+      g[jj] = s8[jj];
+    }
+  }
+}
+
 // Fragment b's len[b] bytes from src + src_off[b] (16-byte aligned) to dst + (the lengths of
 // fragments 0..b-1, one lane each: nfrag <= 64) at any alignment: aligned 16-byte stores of
 // byte-shifted units, the partial units at both ends by bytes (they share a 16-byte unit with the
@@ -427,43 +463,56 @@ __global__ __launch_bounds__(256) void k_gather16(const uint8_t* __restrict__ sr
   }
   __syncthreads();
   if (sh[1]) return;
-  const uint4* s16 = reinterpret_cast<const uint4*>(src + src_off[b]);
-  const uint8_t* s8 = src + src_off[b];
-  uint8_t* const g = dst + sh[0];
-  const uint32_t n = len[b];
-  const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
-  const uint32_t u0 = ad ? 1u : 0u, u1 = (n + ad) >> 4;  // whole units [u0, u1); unit u = bytes [16u - ad, +16)
-  uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
-  const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;
-  const uint32_t stride = blockDim.x * gridDim.y;
-  for (uint32_t u = u0 + blockIdx.y * blockDim.x + threadIdx.x; u < u1; u += stride) {
-    const uint32_t j = 16 * u - ad;
-    const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
-    const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-    uint32_t r5[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      uint32_t vv = x[q];
-#pragma unroll
-      for (int dd = 1; dd < 4; ++dd) vv = dw == (uint32_t)dd ? x[q + dd] : vv;
-      r5[q] = vv;
+  gather_unit(src + src_off[b], len[b], dst + sh[0], blockIdx.y, gridDim.y);
+}
+
+// k_gather16 for the parts of k_compress_sc_span: unit u = part u % parts of block u / parts (one
+// lane each: nblk * parts <= 64, parts a power of 2), at src + out_off[block] + part pitch; a block's
+// parts summed over its lanes by butterfly.  tot[1] = 1: an error mark or an over-long part; 2: a
+// block's parts sum to more than one literal of the block.  Either way nothing is copied.
+__global__ __launch_bounds__(256) void k_gather_parts(const uint8_t* __restrict__ src, const uint64_t* out_off,
+                                                      ScSpan sp, const uint32_t* in_len, uint32_t nunit,
+                                                      uint64_t* tot, uint8_t* __restrict__ dst) {
+  __shared__ uint32_t sh[2];
+  const uint32_t u = blockIdx.x;
+  if (threadIdx.x < kWave) {
+    const uint32_t l = threadIdx.x;
+    const uint32_t L = l < nunit ? sp.part_len[l] : 0u;
+    const bool big = L > 0x20000u;  // error marks (>= 0xfff00000); a part is <= 80 KiB, a screened literal <= 64 KiB + 5
+    const uint32_t Lv = big ? 0u : L;
+    uint32_t sum = Lv;  // the block's parts
+    for (uint32_t d = 1; d < sp.parts; d <<= 1) sum += (uint32_t)__shfl_xor((int)sum, (int)d, 64);
+    const uint32_t nb = l < nunit ? in_len[l / sp.parts] : 0u;
+    const bool over = l < nunit && l % sp.parts == 0 && nb && sum > literal_tag_bytes(nb) + nb;
+    const uint32_t before = scan_dpp(l < u ? Lv : 0u);
+    const uint32_t all = scan_dpp(Lv);
+    const uint32_t code = ballot(big) ? 1u : (ballot(over) ? 2u : 0u);
+    if (l == 63) {
+      sh[0] = before;
+      sh[1] = code;
+      if (u == 0 && blockIdx.y == 0) {
+        tot[0] = all;
+        tot[1] = code;
+      }
     }
-    g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
-                        __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
   }
-  if (blockIdx.y == 0) {
-    const uint32_t nh = min(u0 ? 16 - ad : 0u, n);
-    const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);
-    if (threadIdx.x < nh + (n - tb)) {
-      const uint32_t jj = threadIdx.x < nh ? threadIdx.x : tb + (threadIdx.x - nh);
-      g[jj] = s8[jj];
-    }
-  }
+  __syncthreads();
+  if (sh[1]) return;
+  const uint32_t b = u / sp.parts, j = u % sp.parts;
+  gather_unit(src + out_off[b] + (uint64_t)j * sp.pitch, sp.part_len[u], dst + sh[0], blockIdx.y, gridDim.y);
 }
 
 hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,
                             uint64_t* out_off, hipStream_t s) {
   hipLaunchKernelGGL(k_frag_plan, dim3((nfrag + 255) / 256), dim3(256), 0, s, n, nfrag, slot, in_off, in_len, out_off);
+  return hipGetLastError();
+}
+
+hipError_t launch_parts_gather(const uint8_t* src, const uint64_t* out_off, const ScSpan& sp, const uint32_t* in_len,
+                               uint32_t nblk, uint64_t* tot, uint8_t* dst, hipStream_t s) {
+  const uint32_t nunit = nblk * sp.parts;
+  if (nblk == 0 || sp.parts == 0 || (sp.parts & (sp.parts - 1)) || nunit > kWave) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gather_parts, dim3(nunit, 4), dim3(256), 0, s, src, out_off, sp, in_len, nunit, tot, dst);
   return hipGetLastError();
 }
 

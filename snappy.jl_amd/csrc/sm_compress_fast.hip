@@ -176,4 +176,15 @@ hipError_t launch_compress_fast(const CompressArgs& a0, int mode, hipStream_t s)
   return launch_compress_sc(a, mode, s);
 }
 
+// the screen, then the parse in parts (k_compress_sc_span)
+hipError_t launch_compress_span(const CompressArgs& a0, int mode, const ScSpan& sp, hipStream_t s) {
+  if (mode != 1 && mode != 2) return hipErrorInvalidValue;
+  CompressArgs a = a0;
+  a.screened = 1;
+  hipLaunchKernelGGL(k_literal_screen, dim3(a.nblk), dim3(kScrThreads), 0, s, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_compress_sc_span(a, mode, sp, s);
+}
+
 }  // namespace sm

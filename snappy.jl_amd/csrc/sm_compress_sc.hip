@@ -130,6 +130,7 @@ struct ScLds {
 static_assert(sizeof(ScLds) <= 160 * 1024, "LDS");
 static_assert(sizeof(ScWaveLds) % 16 == 0 && offsetof(ScLds, w) % 16 == 0, "rows are 16-byte aligned");
 static_assert(kScSlot % 16 == 0 && offsetof(ScLds, ring) % 16 == 0, "slots are 16-byte aligned");
+static_assert(kScSlot == kSpanSlot, "the host sizes part pitches by the staging slot");
 
 // wait (bounded) until the LDS word at p satisfies pred; false if the wait gave up
 template <typename Pred>
@@ -785,16 +786,18 @@ __device__ __attribute__((always_inline)) inline void sc_copy_out(uint8_t* const
   }
 }
 
-// The writer wave: the staged super-chunks in order, each at the running output offset (no wave
-// waits for another's offset), then the block's length.  A block whose parse came out larger than
-// one literal of the whole block (a nearly incompressible block past the screen) is rewritten as
-// that literal (emit_literal!, internal.jl:271-284): the output never exceeds the literal size.
-__device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, const CompressArgs& a, uint32_t b, uint32_t n,
-                                                               uint8_t* const dst, uint32_t hv, uint32_t nsc,
-                                                               uint32_t lane) {
+// The writer wave: the staged super-chunks k0..k1-1 in order, each at the running output offset (no
+// wave waits for another's offset), then the output's length into *len_out.  A whole block
+// (whole) whose parse came out larger than one literal of the block (a nearly incompressible block
+// past the screen) is rewritten as that literal (emit_literal!, internal.jl:271-284): the output
+// never exceeds the literal size.  (A part of a block, k_compress_sc_span: the gather checks its
+// block's sum instead.)
+__device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, uint32_t n, uint8_t* const dst, uint32_t hv,
+                                                               uint32_t k0, uint32_t k1, bool whole,
+                                                               uint32_t* len_out, uint32_t lane) {
   uint32_t o = hv, err = 0;
   STAMP_DECL
-  for (uint32_t k = 0; k < nsc; ++k) {
+  for (uint32_t k = k0; k < k1; ++k) {
     const uint32_t slot = k % kScRing;
     const uint32_t sz = sc_wait(&S.rsize[slot], [](uint32_t v) { return v != 0; }, err, 4u) - 1;
     STAMP(8)
@@ -807,7 +810,7 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, const 
     __hip_atomic_store(&S.rseq[slot], k + kScRing, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   const uint32_t h = hv + (n ? literal_tag_bytes(n) : 0u);
-  if (!err && n && o > h + n) {  // one literal: the tag after the varint, the block from LDS
+  if (whole && !err && n && o > h + n) {  // one literal: the tag after the varint, the block from LDS
     uint8_t* const g = dst + hv;
     const uint32_t tb = h - hv, len = tb + n;  // literal stream bytes j: the tag (j < tb), then blk[j - tb]
     const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
@@ -830,7 +833,7 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, const 
     o = h + n;
   }
   err |= uniform(__hip_atomic_load(&S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-  if (lane == 0) a.out_len[b] = err ? 0xfff00000u | err : o;  // (an error mark: > any block's length)
+  if (lane == 0) *len_out = err ? 0xfff00000u | err : o;  // (an error mark: > any block's length)
   STAMP_FLUSH(g_stamp_sc)
 }
 
@@ -914,7 +917,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
     const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, (int)n, 0x00020000);
     if (wave == kScWorkers) {
       __builtin_amdgcn_s_setprio(SC_WPRIO);  // (the writer's chain gates the slots)
-      sc_writer(S, a, b, n, dst, hv, nsc, lane);
+      sc_writer(S, n, dst, hv, 0, nsc, true, &a.out_len[b], lane);
       __builtin_amdgcn_s_setprio(0);
     } else {
       // (no lane-0-only code here or at the end of a super-chunk: the compiler merged two such
@@ -931,6 +934,116 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
     b = bn;
   }
 #undef SC_FETCH
+}
+
+// ---- one block in parts, for latency (sm_compress of small inputs) ------------------------
+// Item i = (block i / parts, part j = i % parts) parses super-chunks [j span, (j + 1) span) of its
+// block on its own workgroup, so a few blocks use many CUs.  The parse of a super-chunk depends on
+// the block's bytes and the table state before it (every earlier position inserted in order), so
+// the item first rebuilds that state: a slot ends up holding the LATEST earlier position of its
+// hash and parity, i.e. the maximum -- order-free, so all waves insert with ds_max_u32: the odd
+// groups' slots (high halves) first, then the even groups' (low halves, the high half read back
+// and kept).  Everything after that is the whole-block kernel's code, so the output equals the
+// concatenation of the block's output in k_compress_sc (sans its literal fallback, which the
+// gather checks per block).  Item outputs at out + out_off[block] + j pitch, lengths in
+// part_len[i]; a block the screen emitted as a literal has that literal as its part 0.
+template <int kDense>
+__global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a, ScSpan sp) {
+  __shared__ __attribute__((aligned(16))) ScLds S;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = uniform(tid >> 6);
+  const uint32_t lane = tid & 63;
+  const uint32_t b = blockIdx.x / sp.parts, j = blockIdx.x % sp.parts;
+  if (b >= a.nblk) return;
+  uint32_t* const plen = sp.part_len + blockIdx.x;
+  const uint32_t n = a.in_len[b];
+  if (n > kBlockSize) {  // not a block: an error mark in part 0 (the gather refuses it)
+    if (tid == 0) *plen = j == 0 ? 0xffffffffu : 0u;
+    return;
+  }
+  const uint32_t nsc = (n + kScS - 1) / kScS;
+  const uint32_t k0 = j * sp.span, k1 = min(k0 + sp.span, nsc);
+  const bool todo = !a.screened || a.out_len[b] == kScreenTodoSc;
+  if (!todo || k0 >= k1) {  // a screened literal (part 0 is its output) or a part past the block
+    if (tid == 0) *plen = (!todo && j == 0) ? a.out_len[b] : 0u;
+    return;
+  }
+  const uint8_t* const src = a.in + a.in_off[b];
+  uint8_t* const dst = a.out + a.out_off[b] + (uint64_t)j * sp.pitch;
+  // ---- stage the block, clear the table (as k_compress_sc) ----
+  if (((uintptr_t)src & 15) == 0) {
+    const uint4* s16 = reinterpret_cast<const uint4*>(src);
+    uint4* d16 = reinterpret_cast<uint4*>(S.blk);
+    const uint32_t n16 = n >> 4;
+    for (uint32_t k = tid; k < n16; k += kScThreads) d16[k] = s16[k];
+    for (uint32_t k = (n & ~15u) + tid; k < n; k += kScThreads) S.blk[k] = src[k];
+  } else {
+    for (uint32_t k = tid; k < n; k += kScThreads) S.blk[k] = src[k];
+  }
+  if (tid < 64) S.blk[n + tid] = 0;
+  {
+    uint4* t16 = reinterpret_cast<uint4*>(S.T);
+    for (uint32_t k = tid; k < 4 * kScTabWords / 16; k += kScThreads) t16[k] = make_uint4(0, 0, 0, 0);
+  }
+  const uint32_t hv = (a.header && j == 0) ? varint_len(n) : 0u;
+  if (tid < hv) dst[tid] = (uint8_t)(((n >> (7 * tid)) & 0x7f) | (tid + 1 < hv ? 0x80 : 0));
+  if (wave == 0) {  // the hand-off words, starting at super-chunk k0
+    if (lane < kScRing) {
+      S.rsize[lane] = 0;
+      S.rseq[lane] = k0 + ((lane - k0) & (kScRing - 1));
+    }
+    if (lane == 0) {
+      S.ins = k0;
+      S.next = 64 * k0;
+      S.err = 0;
+    }
+  }
+  __syncthreads();
+  // ---- the table as the in-order insert of positions [0, kScS k0) leaves it (section B's values:
+  // position + 1, group parity = slot; positions without 4 bytes before the block end never enter)
+  const uint32_t pe = kScS * k0;
+  for (int ph = 1; ph >= 0; --ph) {
+    for (uint32_t G = 2 * wave + (uint32_t)ph; 64 * G < pe; G += 2 * kScW) {
+      const uint32_t q = 64 * G + lane;
+      if (q + 4 <= n) {
+        const uint32_t qa = q & ~3u;
+        const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, qa + 4), sc_ld32(S.blk, qa), q & 3u);
+        uint32_t* const t = &S.T[(w * kHashMul) >> (32 - kScTabBits)];
+        if (ph) {
+          __hip_atomic_fetch_max(t, (q + 1) << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {  // (the high half is final: only low halves change in this phase)
+          const uint32_t hi = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & 0xffff0000u;
+          __hip_atomic_fetch_max(t, hi | (q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, (int)n, 0x00020000);
+  if (wave == kScWorkers) {
+    __builtin_amdgcn_s_setprio(SC_WPRIO);
+    sc_writer(S, n, dst, hv, k0, k1, false, plen, lane);
+    __builtin_amdgcn_s_setprio(0);
+  } else {
+    for (;;) {
+      const uint32_t k = uniform(__hip_atomic_fetch_add(&S.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 6;
+      if (k >= k1) break;
+      sc_superchunk<kDense>(S, k, n, wave, lane, gb);
+    }
+  }
+}
+
+hipError_t launch_compress_sc_span(const CompressArgs& a, int mode, const ScSpan& sp, hipStream_t s) {
+  if (sp.parts == 0 || sp.span == 0 || sp.parts * sp.span < (kBlockSize + kScS - 1) / kScS ||
+      sp.pitch < (uint64_t)sp.span * kScSlot)
+    return hipErrorInvalidValue;
+  const uint32_t grid = a.nblk * sp.parts;
+  if (grid == 0) return hipSuccess;
+  if (mode == 2)
+    hipLaunchKernelGGL(k_compress_sc_span<1>, dim3(grid), dim3(kScThreads), 0, s, a, sp);
+  else
+    hipLaunchKernelGGL(k_compress_sc_span<0>, dim3(grid), dim3(kScThreads), 0, s, a, sp);
+  return hipGetLastError();
 }
 
 #if SM_STAMP
