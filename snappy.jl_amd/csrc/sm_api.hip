@@ -88,7 +88,7 @@ struct sm_ctx {
   HostBuf stage;
   int last_path = -1;  // sm_ctx_last_path
   bool small = true;   // sm_ctx_set_small_decode
-  bool split = false;  // sm_ctx_set_split_compress
+  bool split = true;   // sm_ctx_set_split_compress
   bool last_split = false;  // the last sm_compress parsed its fragments in parts
   std::mutex mu;       // serialises the host-buffer entry points (they share the scratch above)
 };
@@ -887,7 +887,7 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   SM_CHECK(ctx->in.ensure(n + 16));
   SM_CHECK(ctx->out.ensure((size_t)nfrag * slot));
   SM_CHECK(ctx->out2.ensure(sm_max_compressed_length(n) + 16));
-  SM_CHECK(ctx->meta.ensure((size_t)nfrag * 32 + 64 + 4 * sm::kWave));
+  SM_CHECK(ctx->meta.ensure((size_t)nfrag * 32 + 64 + 4 * 256));
   uint8_t* m = (uint8_t*)ctx->meta.p;
   uint64_t* d_in_off = (uint64_t*)m;
   uint64_t* d_out_off = (uint64_t*)(m + 8 * (size_t)nfrag);
@@ -900,50 +900,44 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
   // prefix sums) on the device; the gather kernel writes the stream body into the context's
   // pinned staging (device-mapped: no copy engine behind the kernels), copied out on the host.
   // The fast modes parse each fragment in parts on their own workgroups (k_compress_sc_span: the
-  // same bytes, a fraction of one block's latency); a fragment whose parts would have become one
-  // literal in the whole-block parse (tot[1] == 2) sends the call through the whole-block parse.
+  // same bytes, a fraction of one block's latency; up to 256 parts in all, one per CU).
   const size_t t_off = align_up(sm_max_compressed_length(n) + 16, 256);
   if (n <= kSmallCompressMax && ctx->stage.ensure(t_off + 16) == hipSuccess && ctx->stage.dp) {
     uint32_t parts = 1;
     if (mode != SM_MODE_REFERENCE && ctx->split) {
       uint32_t p2 = 1;
       while (p2 < nfrag) p2 <<= 1;
-      parts = sm::kWave / p2;  // nfrag * parts <= 64 gather units; >= 1
+      parts = std::min<uint32_t>(sm::kWave, 256 / p2);  // nfrag * parts <= 256 gather units
     }
     const uint32_t span = (uint32_t)((SM_BLOCK_SIZE / 1024 + parts - 1) / parts);
-    const size_t pslot = std::max<size_t>(slot, (size_t)parts * span * sm::kSpanSlot);
-    SM_CHECK(ctx->out.ensure((size_t)nfrag * pslot));
+    const size_t sl = parts > 1 ? std::max<size_t>(slot, (size_t)parts * span * sm::kSpanSlot) : slot;
+    SM_CHECK(ctx->out.ensure((size_t)nfrag * sl));
     SM_CHECK(hipMemcpyAsync(ctx->in.p, input, n, hipMemcpyHostToDevice, s));
+    SM_CHECK(sm::launch_frag_plan(n, nfrag, sl, d_in_off, d_in_len, d_out_off, s));
+    sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
+                       nfrag, sm::hashtable_size(n), 0};
+    // the gather writes the body and its (length, error) pair straight into the pinned staging
     uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
-    const volatile uint64_t* tot = (const volatile uint64_t*)((uint8_t*)ctx->stage.p + t_off);
-    for (int whole = parts > 1 ? 0 : 1; whole < 2; ++whole) {
-      const size_t sl = whole ? slot : pslot;
-      SM_CHECK(sm::launch_frag_plan(n, nfrag, sl, d_in_off, d_in_len, d_out_off, s));
-      sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
-                         nfrag, sm::hashtable_size(n), 0};
-      // the gather writes the body and its (length, error) pair straight into the pinned staging
-      if (whole) {
-        SM_CHECK(sm::launch_compress(a, mode, s));
-        SM_CHECK(sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag,
-                                        (uint64_t*)(sdp + t_off), sdp, s));
-      } else {
-        const sm::ScSpan sp{parts, span, (uint64_t)span * sm::kSpanSlot, d_part_len};
-        SM_CHECK(sm::launch_compress_span(a, mode, sp, s));
-        SM_CHECK(sm::launch_parts_gather((const uint8_t*)ctx->out.p, d_out_off, sp, d_in_len, nfrag,
-                                         (uint64_t*)(sdp + t_off), sdp, s));
-      }
-      SM_CHECK(hipStreamSynchronize(s));
-      HT("compress (small): all")
-      if (!whole && tot[1] == 2) continue;  // a fragment the whole-block parse emits as one literal
-      const uint64_t len = tot[0];
-      if (tot[1]) return SM_ERR_DEVICE;  // a block's error mark (SM_OUT_LEN_ERROR), never expected
-      if (hl + len > *compressed_length) return SM_BUFFER_TOO_SMALL;
-      memcpy(compressed + hl, ctx->stage.p, len);
-      *compressed_length = hl + len;
-      ctx->last_split = !whole;
-      return SM_OK;
+    if (parts > 1) {
+      const sm::ScSpan sp{parts, span, (uint64_t)span * sm::kSpanSlot, d_part_len};
+      SM_CHECK(sm::launch_compress_span(a, mode, sp, s));
+      SM_CHECK(sm::launch_parts_gather((const uint8_t*)ctx->out.p, d_out_off, sp, (const uint8_t*)ctx->in.p,
+                                       d_in_off, d_in_len, nfrag, (uint64_t*)(sdp + t_off), sdp, s));
+    } else {
+      SM_CHECK(sm::launch_compress(a, mode, s));
+      SM_CHECK(sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag,
+                                      (uint64_t*)(sdp + t_off), sdp, s));
     }
-    return SM_ERR_DEVICE;  // (not reached: the whole-block round returns)
+    SM_CHECK(hipStreamSynchronize(s));
+    HT("compress (small): all")
+    const volatile uint64_t* tot = (const volatile uint64_t*)((uint8_t*)ctx->stage.p + t_off);
+    const uint64_t len = tot[0];
+    if (tot[1]) return SM_ERR_DEVICE;  // a block's error mark (SM_OUT_LEN_ERROR), never expected
+    if (hl + len > *compressed_length) return SM_BUFFER_TOO_SMALL;
+    memcpy(compressed + hl, ctx->stage.p, len);
+    *compressed_length = hl + len;
+    ctx->last_split = parts > 1;
+    return SM_OK;
   }
   SM_CHECK(hipMemcpyAsync(d_in_off, in_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));
   SM_CHECK(hipMemcpyAsync(d_out_off, out_off.data(), 8 * (size_t)nfrag, hipMemcpyHostToDevice, s));

@@ -467,39 +467,55 @@ __global__ __launch_bounds__(256) void k_gather16(const uint8_t* __restrict__ sr
 }
 
 // k_gather16 for the parts of k_compress_sc_span: unit u = part u % parts of block u / parts (one
-// lane each: nblk * parts <= 64, parts a power of 2), at src + out_off[block] + part pitch; a block's
-// parts summed over its lanes by butterfly.  tot[1] = 1: an error mark or an over-long part; 2: a
-// block's parts sum to more than one literal of the block.  Either way nothing is copied.
+// thread each: nblk * parts <= 256, parts a power of 2 <= 64, so a block's parts are lanes of one
+// wave, summed by butterfly), at src + out_off[block] + part pitch.  A block whose parts sum to more
+// than one literal of the block is written as that literal instead (emit_literal!,
+// internal.jl:271-284: the whole-block parse's fallback, k_compress_sc's writer), from the input.
+// tot[0] = the total; tot[1] = 1 on an error mark (nothing is copied).
 __global__ __launch_bounds__(256) void k_gather_parts(const uint8_t* __restrict__ src, const uint64_t* out_off,
-                                                      ScSpan sp, const uint32_t* in_len, uint32_t nunit,
+                                                      ScSpan sp, const uint8_t* __restrict__ in,
+                                                      const uint64_t* in_off, const uint32_t* in_len, uint32_t nunit,
                                                       uint64_t* tot, uint8_t* __restrict__ dst) {
-  __shared__ uint32_t sh[2];
-  const uint32_t u = blockIdx.x;
-  if (threadIdx.x < kWave) {
-    const uint32_t l = threadIdx.x;
-    const uint32_t L = l < nunit ? sp.part_len[l] : 0u;
-    const bool big = L > 0x20000u;  // error marks (>= 0xfff00000); a part is <= 80 KiB, a screened literal <= 64 KiB + 5
-    const uint32_t Lv = big ? 0u : L;
-    uint32_t sum = Lv;  // the block's parts
-    for (uint32_t d = 1; d < sp.parts; d <<= 1) sum += (uint32_t)__shfl_xor((int)sum, (int)d, 64);
-    const uint32_t nb = l < nunit ? in_len[l / sp.parts] : 0u;
-    const bool over = l < nunit && l % sp.parts == 0 && nb && sum > literal_tag_bytes(nb) + nb;
-    const uint32_t before = scan_dpp(l < u ? Lv : 0u);
-    const uint32_t all = scan_dpp(Lv);
-    const uint32_t code = ballot(big) ? 1u : (ballot(over) ? 2u : 0u);
-    if (l == 63) {
-      sh[0] = before;
-      sh[1] = code;
-      if (u == 0 && blockIdx.y == 0) {
-        tot[0] = all;
-        tot[1] = code;
-      }
-    }
-  }
+  __shared__ uint32_t wsum[4], ex[256], eff[256], code;
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const uint32_t L = t < nunit ? sp.part_len[t] : 0u;
+  const bool big = L > 0x20000u;  // error marks (>= 0xfff00000); a part is <= 80 KiB, a screened literal <= 64 KiB + 5
+  const uint32_t Lv = big ? 0u : L;
+  uint32_t sum = Lv;  // the block's parts
+  for (uint32_t d = 1; d < sp.parts; d <<= 1) sum += (uint32_t)__shfl_xor((int)sum, (int)d, 64);
+  const uint32_t nb = t < nunit ? in_len[t / sp.parts] : 0u;
+  const uint32_t lit = nb ? literal_tag_bytes(nb) + nb : 0u;
+  const bool over = t < nunit && nb && sum > lit;
+  const uint32_t E = over ? (t % sp.parts == 0 ? lit : 0u) : Lv;  // this unit's bytes in the stream
+  const uint32_t inc = scan_dpp(E);
+  const uint64_t anybig = ballot(big);
+  if (t == 0) code = 0;
+  if (lane == 63) wsum[w] = inc;
   __syncthreads();
-  if (sh[1]) return;
+  if (lane == 0 && anybig) code = 1;
+  uint32_t pre = 0;
+  for (uint32_t k = 0; k < w; ++k) pre += wsum[k];
+  ex[t] = pre + inc - E;
+  eff[t] = over ? 1u : 0u;
+  __syncthreads();
+  const uint32_t u = blockIdx.x;
+  if (u == 0 && blockIdx.y == 0 && t == 0) {
+    tot[0] = (uint64_t)wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    tot[1] = code;
+  }
+  if (code) return;
   const uint32_t b = u / sp.parts, j = u % sp.parts;
-  gather_unit(src + out_off[b] + (uint64_t)j * sp.pitch, sp.part_len[u], dst + sh[0], blockIdx.y, gridDim.y);
+  uint8_t* const g = dst + ex[u];
+  if (!eff[u]) {
+    gather_unit(src + out_off[b] + (uint64_t)j * sp.pitch, sp.part_len[u], g, blockIdx.y, gridDim.y);
+  } else if (j == 0) {  // the block as one literal: its tag, then its bytes
+    const uint32_t n = in_len[b], tb = literal_tag_bytes(n);
+    if (blockIdx.y == 0 && t < tb) {
+      const uint32_t n1 = n - 1;
+      g[t] = tb == 1 ? (uint8_t)(n1 << 2) : (t == 0 ? (uint8_t)((58 + tb) << 2) : (uint8_t)(n1 >> (8 * (t - 1))));
+    }
+    gather_unit(in + in_off[b], n, g + tb, blockIdx.y, gridDim.y);
+  }
 }
 
 hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,
@@ -508,11 +524,14 @@ hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t*
   return hipGetLastError();
 }
 
-hipError_t launch_parts_gather(const uint8_t* src, const uint64_t* out_off, const ScSpan& sp, const uint32_t* in_len,
-                               uint32_t nblk, uint64_t* tot, uint8_t* dst, hipStream_t s) {
+hipError_t launch_parts_gather(const uint8_t* src, const uint64_t* out_off, const ScSpan& sp, const uint8_t* in,
+                               const uint64_t* in_off, const uint32_t* in_len, uint32_t nblk, uint64_t* tot,
+                               uint8_t* dst, hipStream_t s) {
   const uint32_t nunit = nblk * sp.parts;
-  if (nblk == 0 || sp.parts == 0 || (sp.parts & (sp.parts - 1)) || nunit > kWave) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_gather_parts, dim3(nunit, 4), dim3(256), 0, s, src, out_off, sp, in_len, nunit, tot, dst);
+  if (nblk == 0 || sp.parts == 0 || sp.parts > kWave || (sp.parts & (sp.parts - 1)) || nunit > 256)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_gather_parts, dim3(nunit, 4), dim3(256), 0, s, src, out_off, sp, in, in_off, in_len, nunit,
+                     tot, dst);
   return hipGetLastError();
 }
 

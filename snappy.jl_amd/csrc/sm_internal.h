@@ -99,9 +99,10 @@ hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t s
 hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,
                             uint64_t* out_off, hipStream_t s);
 // Fast modes, small inputs, for latency: each block parsed in `parts` parts of `span` 1 KiB
-// super-chunks on their own workgroups (k_compress_sc_span; the same bytes as the whole-block
-// parse).  Part j of block b writes at out + out_off[b] + j pitch (pitch >= span kSpanSlot) and its
-// length to part_len[b parts + j]; parts * span >= 64.  Runs the screen first.
+// super-chunks on their own workgroups (k_compress_sc_span; with launch_parts_gather, the same
+// bytes as the whole-block parse).  Part j of block b writes at out + out_off[b] + j pitch (pitch >=
+// span kSpanSlot) and its length to part_len[b parts + j]; parts * span >= 64.  Runs the screen
+// first.
 constexpr uint32_t kSpanSlot = 1280;  // a super-chunk's output bound (k_compress_sc's staging slot)
 struct ScSpan {
   uint32_t parts, span;
@@ -110,12 +111,12 @@ struct ScSpan {
 };
 hipError_t launch_compress_span(const CompressArgs& a, int mode, const ScSpan& sp, hipStream_t s);
 hipError_t launch_compress_sc_span(const CompressArgs& a, int mode, const ScSpan& sp, hipStream_t s);  // (no screen)
-// The parts of nblk (<= 64 / parts) blocks behind one another into dst: tot[0] = the total, tot[1] =
-// 1 on an error mark or a length over its bound (nothing copied), 2 when a block's parts sum to
-// more than one literal of the block (the whole-block parse would have emitted that literal: the
-// caller redoes the call without parts; nothing copied).
-hipError_t launch_parts_gather(const uint8_t* src, const uint64_t* out_off, const ScSpan& sp, const uint32_t* in_len,
-                               uint32_t nblk, uint64_t* tot, uint8_t* dst, hipStream_t s);
+// The parts of nblk (<= 256 / parts) blocks behind one another into dst (a block whose parts sum to
+// more than one literal of the block -- the whole-block parse's fallback -- as that literal, from
+// in): tot[0] = the total, tot[1] = 1 on an error mark or an over-long part (nothing copied).
+hipError_t launch_parts_gather(const uint8_t* src, const uint64_t* out_off, const ScSpan& sp, const uint8_t* in,
+                               const uint64_t* in_off, const uint32_t* in_len, uint32_t nblk, uint64_t* tot,
+                               uint8_t* dst, hipStream_t s);
 hipError_t launch_frag_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* out_len,
                               const uint32_t* in_len, uint32_t nfrag, uint64_t* tot, uint8_t* dst, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)

@@ -734,16 +734,16 @@ def test_single_calls_through_pinned_staging(sm, oracle, gpu_available):
 def test_compress_in_parts_equals_whole_block_parse(sm, oracle, gpu_available, mode):
     """compress() of small inputs parses each 64 KiB fragment in parts on their own workgroups
     (sm_compress_sc.hip k_compress_sc_span: the table state before a part rebuilt by ds_max of
-    every earlier position).  The bytes must equal the whole-fragment parse's, including inputs
-    whose whole-block parse falls back to one literal (small random fragments: the call redoes
-    itself without parts), fragments ending mid super-chunk, and every fragment count up to 64."""
+    every earlier position).  The bytes must equal the whole-fragment parse's, including fragments
+    whose whole-block parse falls back to one literal (small random fragments: the parts gather
+    writes that literal), fragments ending mid super-chunk, and every fragment count up to 64."""
     rng = np.random.default_rng(0x5BA7)
     text = read_testfile("alice29.txt") + read_testfile("html") + read_testfile("urls.10K")
     cases = []
     for n in (1, 17, 1023, 1024, 1025, 4096 + 7, 12836, 65535, 65536, 65537, 100000, 150001, 300000):
         cases.append(text[:n])
-    cases.append((text * 7)[:(64 << 16)])          # 64 fragments (the largest split count: 1 part each)
-    cases.append((text * 7)[:(33 << 16) + 5])      # 34 fragments: parts = 1 (no split)
+    cases.append((text * 7)[:(64 << 16)])          # 64 fragments: 4 parts each
+    cases.append((text * 7)[:(33 << 16) + 5])      # 34 fragments: 4 parts each
     cases.append(rng.integers(0, 256, 5000, dtype=np.uint8).tobytes())       # parse expands: redo
     cases.append(rng.integers(0, 256, 200000, dtype=np.uint8).tobytes())     # screened literals
     mixed = bytearray(text[:70000])
@@ -754,16 +754,14 @@ def test_compress_in_parts_equals_whole_block_parse(sm, oracle, gpu_available, m
                  "geo.protodata", "smallrandom1.bin"):
         cases.append(read_testfile(name))
     try:
-        redo = 0
         for raw in cases:
             sm.set_split_compress(False)
             whole = sm.compress(raw, mode=mode)
             assert not sm.last_compress_split()
             sm.set_split_compress(True)
             parts = sm.compress(raw, mode=mode)
-            redo += not sm.last_compress_split()
+            assert sm.last_compress_split() == (len(raw) <= (4 << 20) and -(-len(raw) // 65536) <= 128)
             assert parts == whole, len(raw)
             assert oracle.uncompress(parts) == raw
-        assert redo >= 1  # the 5000-byte random input
     finally:
         sm.set_split_compress(True)
