@@ -100,3 +100,27 @@ def test_fast_modes_random_structured_blocks(sm, oracle, gpu_available, seed):
         assert not ost.any(), (mode, np.nonzero(ost)[0][:5])
         assert np.array_equal(olen, lens.astype(np.uint32))
         assert np.array_equal(odec, np.concatenate(blocks)), mode
+
+
+@pytest.mark.parametrize("seed", range(1, 1 + int(os.environ.get("SM_FUZZ_SEEDS", "3"))))
+def test_single_calls_random_structured_inputs(sm, oracle, gpu_available, seed):
+    """The single-buffer calls on multi-fragment inputs built from the same structured blocks
+    (1 B .. ~1 MiB): compress in parts (k_compress_sc_span, parts gather) equals the
+    whole-fragment parse byte for byte in both fast modes, every stream decodes under the oracle,
+    and uncompress (path 4, path 0, pinned-staging results) returns the input."""
+    rng = np.random.default_rng(1000 + seed)
+    text = np.frombuffer(open(os.path.join(TESTDATA, "lcet10.txt"), "rb").read(), np.uint8)
+    try:
+        for _ in range(12):
+            parts = [gen_block(rng, text) for _ in range(int(rng.integers(1, 17)))]
+            raw = np.concatenate(parts).tobytes()
+            for mode in ("fast", "dense"):
+                sm.set_split_compress(False)
+                whole = sm.compress(raw, mode=mode)
+                sm.set_split_compress(True)
+                split = sm.compress(raw, mode=mode)
+                assert split == whole, (mode, len(raw))
+                assert oracle.uncompress(split) == raw
+                assert sm.uncompress(split) == raw
+    finally:
+        sm.set_split_compress(True)
