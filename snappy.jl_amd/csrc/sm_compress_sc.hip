@@ -947,6 +947,11 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
 // concatenation of the block's output in k_compress_sc (sans its literal fallback, which the
 // gather checks per block).  Item outputs at out + out_off[block] + j pitch, lengths in
 // part_len[i]; a block the screen emitted as a literal has that literal as its part 0.
+// Diagnostic builds only (-DSC_SPAN_ABL=bits; invalid output, timing only): 1 no table rebuild,
+// 2 no parse (and no writer), 4 no block staging.
+#ifndef SC_SPAN_ABL
+#define SC_SPAN_ABL 0
+#endif
 template <int kDense>
 __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a, ScSpan sp) {
   __shared__ __attribute__((aligned(16))) ScLds S;
@@ -971,7 +976,8 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
   const uint8_t* const src = a.in + a.in_off[b];
   uint8_t* const dst = a.out + a.out_off[b] + (uint64_t)j * sp.pitch;
   // ---- stage the block, clear the table (as k_compress_sc) ----
-  if (((uintptr_t)src & 15) == 0) {
+  if (SC_SPAN_ABL & 4) {
+  } else if (((uintptr_t)src & 15) == 0) {
     const uint4* s16 = reinterpret_cast<const uint4*>(src);
     uint4* d16 = reinterpret_cast<uint4*>(S.blk);
     const uint32_t n16 = n >> 4;
@@ -1001,7 +1007,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
   __syncthreads();
   // ---- the table as the in-order insert of positions [0, kScS k0) leaves it (section B's values:
   // position + 1, group parity = slot; positions without 4 bytes before the block end never enter)
-  const uint32_t pe = kScS * k0;
+  const uint32_t pe = (SC_SPAN_ABL & 1) ? 0u : kScS * k0;
   for (int ph = 1; ph >= 0; --ph) {
     for (uint32_t G = 2 * wave + (uint32_t)ph; 64 * G < pe; G += 2 * kScW) {
       const uint32_t q = 64 * G + lane;
@@ -1020,7 +1026,9 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
     __syncthreads();
   }
   const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, (int)n, 0x00020000);
-  if (wave == kScWorkers) {
+  if (SC_SPAN_ABL & 2) {
+    if (tid == 0) *plen = 0;
+  } else if (wave == kScWorkers) {
     __builtin_amdgcn_s_setprio(SC_WPRIO);
     sc_writer(S, n, dst, hv, k0, k1, false, plen, lane);
     __builtin_amdgcn_s_setprio(0);

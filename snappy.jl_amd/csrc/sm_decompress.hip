@@ -1420,9 +1420,12 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
   hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(64), 0, s, in, N, ip0, size, nchunks,
                      reinterpret_cast<const uint2*>(rec), deep, path, ctl, rounds);
   hipLaunchKernelGGL(k_origin_fill_dev, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
+  // later launches usually find nothing pending and return at once: a small grid dispatches
+  // faster, and strides over the pointers when some are left
   const uint32_t g1 = min(32768u, max(1u, (size + 255) / 256));
   for (uint32_t r = 0; r < rounds; ++r)
-    hipLaunchKernelGGL(k_small_resolve, dim3(g1), dim3(256), 0, s, in, P, size, ctl, r, out, words);
+    hipLaunchKernelGGL(k_small_resolve, dim3(r == 0 ? g1 : min(g1, 256u)), dim3(256), 0, s, in, P, size, ctl, r, out,
+                       words);
   return hipGetLastError();
 }
 
