@@ -1008,19 +1008,33 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
   // ---- the table as the in-order insert of positions [0, kScS k0) leaves it (section B's values:
   // position + 1, group parity = slot; positions without 4 bytes before the block end never enter)
   const uint32_t pe = (SC_SPAN_ABL & 1) ? 0u : kScS * k0;
+  // (a lane takes four consecutive positions of one group -- two aligned dwords give their four
+  // words -- and a wave four groups of the phase's parity per step)
+  const uint32_t sub = lane & 15, gq = lane >> 4;
   for (int ph = 1; ph >= 0; --ph) {
-    for (uint32_t G = 2 * wave + (uint32_t)ph; 64 * G < pe; G += 2 * kScW) {
-      const uint32_t q = 64 * G + lane;
-      if (q + 4 <= n) {
-        const uint32_t qa = q & ~3u;
-        const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, qa + 4), sc_ld32(S.blk, qa), q & 3u);
-        uint32_t* const t = &S.T[(w * kHashMul) >> (32 - kScTabBits)];
-        if (ph) {
-          __hip_atomic_fetch_max(t, (q + 1) << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {  // (the high half is final: only low halves change in this phase)
-          const uint32_t hi = __hip_atomic_load(t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) & 0xffff0000u;
-          __hip_atomic_fetch_max(t, hi | (q + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
+    for (uint32_t i = wave; 128 * (4 * i) < pe; i += kScW) {
+      const uint32_t G = 2 * (4 * i + gq) + (uint32_t)ph;  // this lane's group
+      const uint32_t q = 64 * G + 4 * sub;
+      if (q >= pe) continue;
+      const uint32_t d0 = sc_ld32(S.blk, q), d1 = sc_ld32(S.blk, q + 4);
+      uint32_t* t[4];
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t w = j ? __builtin_amdgcn_alignbyte(d1, d0, j) : d0;
+        t[j] = &S.T[(w * kHashMul) >> (32 - kScTabBits)];
+      }
+      if (ph) {
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+          if (q + j + 4 <= n) __hip_atomic_fetch_max(t[j], (q + j + 1) << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {  // (the high half is final: only low halves change in this phase)
+        uint32_t hi[4];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) hi[j] = __hip_atomic_load(t[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+          if (q + j + 4 <= n)
+            __hip_atomic_fetch_max(t[j], (hi[j] & 0xffff0000u) | (q + j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     __syncthreads();
