@@ -913,9 +913,14 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
     const size_t sl = parts > 1 ? std::max<size_t>(slot, (size_t)parts * span * sm::kSpanSlot) : slot;
     SM_CHECK(ctx->out.ensure((size_t)nfrag * sl));
     SM_CHECK(hipMemcpyAsync(ctx->in.p, input, n, hipMemcpyHostToDevice, s));
-    SM_CHECK(sm::launch_frag_plan(n, nfrag, sl, d_in_off, d_in_len, d_out_off, s));
     sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
                        nfrag, sm::hashtable_size(n), 0};
+    if (mode == SM_MODE_REFERENCE) {
+      SM_CHECK(sm::launch_frag_plan(n, nfrag, sl, d_in_off, d_in_len, d_out_off, s));
+    } else {  // (the screen, the fast modes' first kernel, writes the fragment table)
+      a.plan_n = n;
+      a.plan_slot = sl;
+    }
     // the gather writes the body and its (length, error) pair straight into the pinned staging
     uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
     if (parts > 1) {

@@ -68,9 +68,24 @@ __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) 
   __shared__ uint32_t cnt[2];
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t b = blockIdx.x;
-  const uint32_t n = a.in_len[b];
-  const uint8_t* src = a.in + a.in_off[b];
-  uint8_t* dst = a.out + a.out_off[b];
+  uint32_t n;
+  uint64_t ioff, ooff;
+  if (a.plan_n) {  // a single-buffer input: this block's fragment-table entry is the screen's to write
+    ioff = (uint64_t)b * kBlockSize;
+    n = (uint32_t)min((uint64_t)kBlockSize, a.plan_n - ioff);
+    ooff = (uint64_t)b * a.plan_slot;
+    if (tid == 0) {
+      const_cast<uint64_t*>(a.in_off)[b] = ioff;
+      const_cast<uint32_t*>(a.in_len)[b] = n;
+      const_cast<uint64_t*>(a.out_off)[b] = ooff;
+    }
+  } else {
+    n = a.in_len[b];
+    ioff = a.in_off[b];
+    ooff = a.out_off[b];
+  }
+  const uint8_t* src = a.in + ioff;
+  uint8_t* dst = a.out + ooff;
   if (n < kScrMinLen || n > kBlockSize) {
     if (tid == 0) a.out_len[b] = kScreenTodo;
     return;

@@ -19,6 +19,11 @@ struct CompressArgs {
   uint32_t table_size;  // 0: per block from its length (internal.jl:107-113); else fixed (Q2)
   int header;           // 1: prefix each block with varint(len) (independent snappy stream)
   int screened;         // set by launch_compress_fast: out_len holds k_literal_screen's verdicts
+  // plan_n != 0 (sm_compress, fast modes): the blocks are the 64 KiB fragments of one input of
+  // plan_n bytes at slot pitch plan_slot, and k_literal_screen writes in_off / in_len / out_off
+  // (instead of a k_frag_plan launch) before the kernels after it read them
+  uint64_t plan_n = 0;
+  uint64_t plan_slot = 0;
 };
 
 struct DecompressArgs {
