@@ -1056,10 +1056,10 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
     }
   }
   ctx->last_path = 0;
-  const uint32_t hm[4] = {0, 0, hv[0], hv[1]};  // d_off (u64 0), d_in_len, d_cap
-  SM_CHECK(hipMemcpyAsync(d_off, hm, 16, hipMemcpyHostToDevice, s));
   sm::DecompressArgs a{(const uint8_t*)ctx->in.p, d_off, d_in_len, (uint8_t*)ctx->out.p, d_off, d_cap, d_out_len,
                        d_status, 1};
+  a.one_n = hv[0];  // (n >= 1 here: the header parsed) -- the stream's length and capacity as arguments
+  a.one_cap = hv[1];
   SM_CHECK(sm::launch_decompress(a, size > SM_BLOCK_SIZE, s));
   // the output (whatever the status) and (out_len, status) into the pinned staging by a kernel
   const size_t w_off = align_up(size, 256);

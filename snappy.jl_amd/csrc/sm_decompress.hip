@@ -614,10 +614,10 @@ __global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a)
   __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];                // output window
   const uint32_t lane = lane_id();
   const uint32_t b = blockIdx.x;
-  const uint8_t* in = a.in + a.in_off[b];
-  const uint32_t N = a.in_len[b];
-  uint8_t* dst = a.out + a.out_off[b];
-  const uint32_t cap = a.out_cap[b];
+  const uint8_t* in = a.one_n ? a.in : a.in + a.in_off[b];
+  const uint32_t N = a.one_n ? a.one_n : a.in_len[b];
+  uint8_t* dst = a.one_n ? a.out : a.out + a.out_off[b];
+  const uint32_t cap = a.one_n ? a.one_cap : a.out_cap[b];
 
   uint32_t size = cap, ip = 0;
   int32_t st = a.raw ? kOk : parse_header(in, N, lane, size, ip);

@@ -37,6 +37,10 @@ struct DecompressArgs {
   int32_t* status;
   uint32_t nblk;
   int raw;  // 1: no varint header -- a fragment of one stream, declared length = out_cap[b]
+  // one_n != 0 (sm_uncompress's in-order path): ONE stream of one_n bytes at in, output capacity
+  // one_cap at out -- in_off / in_len / out_off / out_cap are not read (no upload for them)
+  uint32_t one_n = 0;
+  uint32_t one_cap = 0;
 };
 
 // mode 0 = reference (byte-identical to Snappy.jl), 1 = fast (wave-parallel parse), 2 = fast, denser
