@@ -393,6 +393,8 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   uint8_t* ib = (uint8_t*)ctx->idx.p;
   uint32_t* d_ctl = (uint32_t*)(ib + ctl_off);
   uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
+  // the third verdict word is written by the device only when a pointer stays unresolved
+  ((volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off))[2] = 0;
   if (sm::launch_small_decode((const uint8_t*)ctx->in.p, n, ip0, size, nchunks, (uint32_t*)ib,
                               (sm::OriginPath*)(ib + path_off), d_ctl, (uint32_t*)ctx->org.p, rounds,
                               pin_out ? sdp : (uint8_t*)ctx->out.p, (uint32_t*)(sdp + w_off), s) != hipSuccess)
@@ -400,7 +402,7 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   if (!pin_out && hipMemcpyAsync(host_out, ctx->out.p, size, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
   const volatile uint32_t* w = (const volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off);
-  if (w[0] || w[1] || w[2]) return 0;  // (the last: never, by the round count)
+  if (w[0] || w[1] || w[2]) return 0;  // (w[2]: never, by the round count -- checked, not assumed)
   if (pin_out) memcpy(host_out, ctx->stage.p, size);
   return 4;
 }
@@ -1072,7 +1074,7 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
     const int32_t dst = (int32_t)w[1];
     if (dst != SM_OK) return dst;
     if (dlen > size) return SM_ERR_DEVICE;  // (never: the kernel's bound)
-    memcpy(uncompressed, ctx->stage.p, dlen);
+    if (dlen) memcpy(uncompressed, ctx->stage.p, dlen);  // (uncompressed may be NULL when dlen == 0)
     *uncompressed_length = dlen;
     return SM_OK;
   }

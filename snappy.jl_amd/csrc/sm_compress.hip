@@ -282,7 +282,9 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         h = hash32(cur, shift);
         raw = 0;
         if (__builtin_expect(valid, 1)) raw = tab_probe(stab, h, p);                                // :190 (raw = candidate)
-        hm = ballot(valid && S.word(raw) == cur);                              // :193
+        // (raw < p: a candidate is an earlier position.  The ascending lane order makes that so on
+        // gfx950; the compare makes a different order a missed match, never a wrapped offset)
+        hm = ballot(valid && raw < p && S.word(raw) == cur);                   // :193
         if (hm || ballot(valid) != ~0ull) break;                               // a match, or :175
       }
       const bool found = hm != 0;
@@ -328,7 +330,9 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
           }
         }
         STAMP(2)
-        if (__builtin_expect(f < 4, 0)) break;                                 // :238
+        // :238; cand >= ip (a later position, only if the table's insert order broke) fails as a
+        // verification does: the guard the lane-order assumption lacked
+        if (__builtin_expect(f < 4 || cand >= ip, 0)) break;
         STAMP_COUNT(6, 1)
         // The next candidate first (:228-235, one lane: insert ip-1, read and replace the entry
         // for ip), so the bookkeeping below runs under its LDS round trip.  Past ip_limit the
@@ -464,6 +468,7 @@ __global__ __launch_bounds__(256) void k_gather16(const uint8_t* __restrict__ sr
   __syncthreads();
   if (sh[1]) return;
   gather_unit(src + src_off[b], len[b], dst + sh[0], blockIdx.y, gridDim.y);
+  __threadfence_system();  // (dst: device-mapped host memory, read after the synchronisation)
 }
 
 // k_gather16 for the parts of k_compress_sc_span: unit u = part u % parts of block u / parts (one
@@ -479,12 +484,16 @@ __global__ __launch_bounds__(256) void k_gather_parts(const uint8_t* __restrict_
   __shared__ uint32_t wsum[4], ex[256], eff[256], code;
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
   const uint32_t L = t < nunit ? sp.part_len[t] : 0u;
-  const bool big = L > 0x20000u;  // error marks (>= 0xfff00000); a part is <= 80 KiB, a screened literal <= 64 KiB + 5
+  const uint32_t nb = t < nunit ? in_len[t / sp.parts] : 0u;
+  const uint32_t lit = nb ? literal_tag_bytes(nb) + nb : 0u;
+  // error marks (>= 0xfff00000), and any part longer than its pitch (it would run into the next
+  // part's slot): a part's output is at most span * kSpanSlot = pitch bytes; part 0 may instead be
+  // a screened block's literal (its varint header, tag and bytes)
+  const uint32_t bound = (t % sp.parts == 0) ? max((uint32_t)sp.pitch, lit + 5u) : (uint32_t)sp.pitch;
+  const bool big = t < nunit && L > bound;
   const uint32_t Lv = big ? 0u : L;
   uint32_t sum = Lv;  // the block's parts
   for (uint32_t d = 1; d < sp.parts; d <<= 1) sum += (uint32_t)__shfl_xor((int)sum, (int)d, 64);
-  const uint32_t nb = t < nunit ? in_len[t / sp.parts] : 0u;
-  const uint32_t lit = nb ? literal_tag_bytes(nb) + nb : 0u;
   const bool over = t < nunit && nb && sum > lit;
   const uint32_t E = over ? (t % sp.parts == 0 ? lit : 0u) : Lv;  // this unit's bytes in the stream
   const uint32_t inc = scan_dpp(E);
@@ -516,6 +525,7 @@ __global__ __launch_bounds__(256) void k_gather_parts(const uint8_t* __restrict_
     }
     gather_unit(in + in_off[b], n, g + tb, blockIdx.y, gridDim.y);
   }
+  __threadfence_system();  // (dst: device-mapped host memory, read after the synchronisation)
 }
 
 hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,

@@ -66,10 +66,16 @@ enum : int32_t {
   kErrCopyOffset = 19,
   kErrCopyLength = 20,
   kErrLiteral = 21,
+  kErrDevice = 32,  // SM_ERR_DEVICE: a block length that is a compressor error mark (>= kOutLenError)
   kErrCross = 64,  // internal: a fragment's copy reads another fragment (never returned by the ABI)
 };
 
 __host__ __device__ inline uint32_t max_compressed_length(uint32_t n) { return 32 + n + n / 6; }
+
+// SM_OUT_LEN_ERROR: a compressor's error mark in d_out_len (include/snappy_mi355x.h).  A device
+// decoder handed such a length (a caller passing comp_len straight on) reports kErrDevice without
+// reading the slot: the mark is an error, never a stream length (Snappy.jl:50 raises, never decodes).
+constexpr uint32_t kOutLenError = 0xfff00000u;
 
 // internal.jl:107-113
 __host__ __device__ inline uint32_t hashtable_size(uint64_t n) {

@@ -91,8 +91,9 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
 // rounds u32 (zeroed by the chain kernel) -- ctl[0] path elements, ctl[1] != 0: the chain found no exact path (fall
 // back), ctl[2] != 0: an element failed its checks (fall back), ctl[4 + r] != 0: pointers still
 // unresolved after round r.  P: size u32.  The resolve launches write the output (each quad of
-// bytes in the launch that resolves it) and words[0..2] = ctl[1], ctl[2], 0 (the call's verdict);
-// out and words may be device-mapped pinned host memory.
+// bytes in the launch that resolves it) and words[0..1] = ctl[1], ctl[2]; the last launch sets
+// words[2] = 1 when a pointer is still unresolved after it (the caller zeroes words[2] first).  Any
+// nonzero word: fall back.  out and words may be device-mapped pinned host memory.
 hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
                                uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
                                uint8_t* out, uint32_t* words, hipStream_t s);
