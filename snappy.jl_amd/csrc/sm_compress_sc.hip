@@ -128,7 +128,8 @@ struct ScLds {
   uint32_t err;                        // a hand-off wait timed out (never expected)
 };
 static_assert(sizeof(ScLds) <= 160 * 1024, "LDS");
-static_assert(sizeof(ScWaveLds) % 16 == 0 && offsetof(ScLds, w) % 16 == 0, "rows are 16-byte aligned");
+static_assert(sizeof(ScWaveLds) % 32 == 0 && offsetof(ScLds, w) % 32 == 0 && offsetof(ScWaveLds, O) % 32 == 0,
+              "rows are 32-byte aligned (section C's O addresses XOR the swizzle into bits 2..4)");
 static_assert(kScSlot % 16 == 0 && offsetof(ScLds, ring) % 16 == 0, "slots are 16-byte aligned");
 static_assert(kScSlot == kSpanSlot, "the host sizes part pitches by the staging slot");
 
@@ -164,10 +165,20 @@ __device__ inline uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+// (v_alignbyte_b32 shifts by 8 * S2[1:0]: the shift operands below are byte addresses, unmasked --
+// a `& 3` costs a VALU the compiler does not drop)
+__device__ inline uint32_t sc_abyte(uint32_t hi, uint32_t lo, uint32_t s) { return __builtin_amdgcn_alignbyte(hi, lo, s); }
+
+// the 4 bytes of the block at p (two aligned dwords, one funnel shift)
+__device__ inline uint32_t sc_ld32u(const uint8_t* blk, uint32_t p) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(blk + (p & ~3u));
+  return sc_abyte(w[1], w[0], p);
+}
+
 // 16 bytes of the block at p (five aligned dwords, four funnel shifts)
 __device__ inline uint4 sc_ld128(const uint8_t* blk, uint32_t p) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(blk + (p & ~3u));
-  const uint32_t s = p & 3u;
+  const uint32_t s = p;
   const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
   return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, s), __builtin_amdgcn_alignbyte(w2, w1, s),
                     __builtin_amdgcn_alignbyte(w3, w2, s), __builtin_amdgcn_alignbyte(w4, w3, s));
@@ -226,7 +237,7 @@ __device__ inline uint4 sc_trim(uint4 v, uint32_t len) {
 __device__ inline void sc_lds_or(uint32_t a, uint4 v) {
   // the five dwords from (a - 1) & ~3: alignbyte(hi, lo, t) = (hi:lo) >> 8 (t & 3) with t = 4 - (a & 3),
   // so an aligned a (t = 0) shifts the whole piece one dword up and or-s a zero below it (no selects)
-  const uint32_t wa = (a - 1u) & ~3u, t = (0u - a) & 3u;
+  const uint32_t wa = (a - 1u) & ~3u, t = 0u - a;
   const uint32_t u0 = __builtin_amdgcn_alignbyte(v.x, 0u, t);
   const uint32_t u1 = __builtin_amdgcn_alignbyte(v.y, v.x, t);
   const uint32_t u2 = __builtin_amdgcn_alignbyte(v.z, v.y, t);
@@ -243,7 +254,7 @@ __device__ inline void sc_lds_or(uint32_t a, uint4 v) {
 
 // ors the (up to 3) bytes of cv into the zeroed LDS byte array at byte address a
 __device__ inline void sc_lds_or3(uint32_t a, uint32_t cv) {
-  const uint32_t wa = (a - 1u) & ~3u, t = (0u - a) & 3u;  // (as sc_lds_or)
+  const uint32_t wa = (a - 1u) & ~3u, t = 0u - a;  // (as sc_lds_or)
   const uint32_t lo = __builtin_amdgcn_alignbyte(cv, 0u, t), hi = __builtin_amdgcn_alignbyte(0u, cv, t);
   asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
   if (SC_DUP & 32) asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
@@ -262,6 +273,13 @@ __device__ inline uint32_t sc_lit_tag(uint32_t len, uint32_t& sz) {
   const uint32_t l1 = len - 1;
   sz = len <= 60 ? 1u : (len <= 256 ? 2u : 3u);
   return sz == 1 ? (l1 << 2) : (sz == 2 ? (60u << 2) | (l1 << 8) : (61u << 2) | (l1 << 8));
+}
+
+// lane l: bit l of the lane mask m ? a : b (one v_cndmask on the SGPR pair)
+__device__ inline uint32_t sc_select(uint64_t m, uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+  return r;
 }
 
 // c ? a : b on values (a conditional on lvalues can become a select of their addresses)
@@ -304,7 +322,7 @@ __device__ inline uint32_t sc_ffbl(uint32_t x) {
   return r;
 }
 
-// equal leading bytes (0..16) of the 16 bytes X0..X3 and the 16 bytes at w + s (s < 4; w dword-aligned LDS)
+// equal leading bytes (0..16) of the 16 bytes X0..X3 and the 16 bytes at w + (s & 3) (w dword-aligned LDS)
 __device__ __attribute__((always_inline)) inline uint32_t sc_eq16(uint32_t X0, uint32_t X1, uint32_t X2, uint32_t X3,
                                                                   const uint32_t* w, uint32_t s) {
   const uint32_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3], a4 = w[4];
@@ -316,6 +334,18 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_eq16(uint32_t X0, u
   return min(min(b0, b1), min(min(b2, b3), 128u)) >> 3;
 }
 
+
+// equal leading bytes (0..12) of the 12 bytes at x and at y of the LDS block copy
+__device__ __attribute__((always_inline)) inline uint32_t sc_eq12(const uint8_t* blk, uint32_t x, uint32_t y) {
+  const uint32_t* a = reinterpret_cast<const uint32_t*>(blk + (x & ~3u));
+  const uint32_t* b = reinterpret_cast<const uint32_t*>(blk + (y & ~3u));
+  const uint32_t a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
+  const uint32_t b0 = b[0], b1 = b[1], b2 = b[2], b3 = b[3];
+  const uint32_t f0 = sc_ffbl(sc_abyte(a1, a0, x) ^ sc_abyte(b1, b0, y));
+  const uint32_t f1 = sc_ffbl(sc_abyte(a2, a1, x) ^ sc_abyte(b2, b1, y)) | 32u;
+  const uint32_t f2 = sc_ffbl(sc_abyte(a3, a2, x) ^ sc_abyte(b3, b2, y)) | 64u;
+  return min(min(f0, f1), min(f2, 96u)) >> 3;
+}
 
 // bits [a, b) of a u32 (0 <= a <= b <= 31)
 __device__ inline uint32_t sc_bits(uint32_t a, uint32_t b) { return ((1u << b) - 1u) & ~((1u << a) - 1u); }
@@ -357,11 +387,13 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   // so the loads take immediate offsets; only the block's last super-chunk has positions whose 4
   // bytes run past the block, and only it checks them)
   uint32_t ha[kScG], hvv[kScG], wq[kScG];
-  const uint32_t ql = sc0 + lane, qa = ql & ~3u, qb = ql & 3u;
-  const uint32_t hv0 = ql + 1, hv1 = (ql + 1) << 16;
+  const uint32_t ql = sc0 + lane, qa = ql & ~3u, qb = ql;
+  // (slots hold positions: a never-written slot reads as candidate 0, which the reference's table
+  // gives too, Snappy.jl:30 -- a real candidate, verified like any other)
+  const uint32_t hv0 = ql, hv1 = ql << 16;
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
-    const uint32_t w = __builtin_amdgcn_alignbyte(sc_ld32(S.blk, qa + 64 * g + 4), sc_ld32(S.blk, qa + 64 * g), qb);
+    const uint32_t w = sc_abyte(sc_ld32(S.blk, qa + 64 * g + 4), sc_ld32(S.blk, qa + 64 * g), qb);
     if (SC_DUP & 64) sc_dup2(lds_addr(S.blk + qa + 64 * g));
     wq[g] = w;
     ha[g] = Tbase + 4 * ((w * kHashMul) >> (32 - kScTabBits));
@@ -432,61 +464,68 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   // ratio 0.5625 against 0.5738 on the bench text, but 3.21 against 2.96 ms, and a round trip
   // 3.6% slower: DESIGN.md section 3.2d.) ----
   uint64_t mbs[kScG];
+  // a position's O entry: row r4 = 4 g + (lane >> 4), entry i = lane & 15, at u16 index 16 r4 + (i ^ 2 (g & 7))
+  // (dword pairs swizzled by the group): byte offset (Orel ^ 4 (g & 7)) + 128 g, Orel = the entry's
+  // unswizzled offset in group 0 (bits 2..4 are 2 i's) -- one XOR a group, 128 g an immediate offset
+  uint8_t* const Ob8 = reinterpret_cast<uint8_t*>(Wl.O);
+  const uint32_t Orel = 32 * (lane >> 4) + 2 * (lane & 15);
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
     const uint32_t q = sc0 + 64 * g + lane;
     const uint32_t sh = 16 * (g & 1);
-    const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // position + 1, 0: none
-    const uint32_t c1 = (SC_ABL & 8) ? 0u : max(ca, cb), c2 = (SC_ABL & 8) ? 0u : min(ca, cb);
-    // A candidate is valid when it is an earlier position: c - 1 < q (unsigned, so 0 = empty
-    // fails too).  The table is cleared per block and filled in position order, so a nonzero
-    // entry is an earlier position whenever the conflicting lanes of one ds_mskor_rtn are
-    // serviced in ascending lane order (observed on gfx950); the compare makes validity
-    // independent of that order, at the cost of the nonzero test it replaces.
-    // Positions without 4 bytes before the block end exchanged with the dummy word, and positions
-    // without 4 bytes before the super-chunk end may not start a copy: the walks' row masks leave
-    // both out (D), so no per-group check here.  The loads of a rejected candidate read the
-    // position itself.
-    const bool ok1 = c1 - 1u < q, ok2 = c2 - 1u < q;
-    const uint32_t p1 = ok1 ? c1 - 1 : q, p2 = ok2 ? c2 - 1 : q;
+    const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // positions
+    const uint32_t c1 = (SC_ABL & 8) ? q : max(ca, cb), c2 = (SC_ABL & 8) ? q : min(ca, cb);
+    // A candidate is valid when it is an earlier position: c < q.  The table is cleared per block
+    // and filled in position order, so every slot value is an earlier position whenever the
+    // conflicting lanes of one ds_mskor_rtn are serviced in ascending lane order (observed on
+    // gfx950); the compare makes validity independent of that order.  Positions
+    // without 4 bytes before the block end exchanged with the dummy word, and positions without 4
+    // bytes before the super-chunk end may not start a copy: the walks' row masks leave both out
+    // (D), so no per-group check here.  (A candidate's loads read inside the block copy whatever
+    // its value: c < 65536.)
+    const bool ok1 = c1 < q, ok2 = c2 < q;
+    const uint32_t d1 = q - c1, d2 = q - c2;  // the offsets
+    uint16_t* const Og = reinterpret_cast<uint16_t*>(Ob8 + (Orel ^ (4u * (g & 7))) + 128u * g);
     const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
     if constexpr (kDense) {
       // dense mode: both candidates compared over 16 bytes, the longer kept, its length stored
       // for the walks; on a tie the SC_FAR rule below (the older when the more recent is near)
       const uint4 X = sc_ld128(S.blk, q);
-      uint32_t lw1 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p1 & ~3u)), p1 & 3u);
-      uint32_t lw2 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p2 & ~3u)), p2 & 3u);
+      uint32_t lw1 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (c1 & ~3u)), c1);
+      uint32_t lw2 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (c2 & ~3u)), c2);
       asm("" : "+v"(lw1), "+v"(lw2));  // (keeps the loads unconditional)
       const uint32_t l1 = ok1 ? lw1 : 0u, l2 = ok2 ? lw2 : 0u;
-      const bool take2 = l2 == l1 ? (l2 >= 4 && q - p1 < (uint32_t)SC_FAR) : l2 > l1;
+      const bool take2 = l2 == l1 ? (l2 >= 4 && d1 < (uint32_t)SC_FAR) : l2 > l1;
       const uint32_t l = take2 ? l2 : l1;
       const uint32_t avail = sce - q;  // (>= 4 where l >= 4: room)
       const uint32_t enc = l < 4 ? 0u : ((l == 16 && avail > 16) ? kScExt : min(l, avail));
-      Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (take2 ? p2 : p1));
+      *Og = (uint16_t)(take2 ? d2 : d1);
       Wl.L[16 * r4 + 4 * ((i >> 2) ^ ((g >> 1) & 3)) + (i & 3)] = (uint8_t)enc;
       mbs[g] = ballot(l >= 4);
     } else {
       uint32_t v1, v2;
       if (SC_GC & 1) {
-        v1 = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)p1, 0, 0);
-        v2 = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)p2, 0, 0);
+        v1 = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)c1, 0, 0);
+        v2 = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)c2, 0, 0);
       } else {
-        v1 = lds_ld32(S.blk, p1);
-        v2 = lds_ld32(S.blk, p2);
+        v1 = sc_ld32u(S.blk, c1);
+        v2 = sc_ld32u(S.blk, c2);
       }
       if (SC_DUP & 2) {
-        sc_dup2(lds_addr(S.blk + (p1 & ~3u)));
-        sc_dup2(lds_addr(S.blk + (p2 & ~3u)));
+        sc_dup2(lds_addr(S.blk + (c1 & ~3u)));
+        sc_dup2(lds_addr(S.blk + (c2 & ~3u)));
       }
       const uint32_t w = wq[g];
       asm("" : "+v"(v1), "+v"(v2));  // (keeps the loads unconditional)
-      const bool m1 = ok1 && v1 == w, m2 = ok2 && v2 == w;
+      // the matches as lane masks (ballots of plain compares, combined by SALU: a ballot of an
+      // and-ed bool costs a v_cndmask + v_cmp, and a select on a combined bool two v_cndmask)
+      const uint64_t M1 = ballot(v1 == w) & ballot(ok1), M2 = ballot(v2 == w) & ballot(ok2);
       // the older candidate when the more recent one is nearer than SC_FAR bytes: a copy whose
       // source is that close often reads the output of the decoder's own batch of tags, which
       // then runs it in order ("Candidates for the decoder")
-      const bool use2 = m2 && (!m1 || q - p1 < (uint32_t)SC_FAR);
-      Wl.O[16 * r4 + 2 * (((i >> 1) ^ (g & 7))) + (i & 1)] = (uint16_t)(q - (use2 ? p2 : p1));
-      mbs[g] = ballot(m1 || m2);
+      const uint64_t U = M2 & (~M1 | ballot(d1 < (uint32_t)SC_FAR));
+      *Og = (uint16_t)sc_select(U, d2, d1);  // (a position without a match: never read)
+      mbs[g] = M1 | M2;
     }
   }
   // the row masks: lane d holds dword d of the 16 group ballots (v_writelane), lane l reads its
@@ -540,13 +579,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
             enc = Lrow[i ^ lsw4];  // (computed in C)
           } else {
             const uint32_t q = c0 + i, off = offAt(i);
-            uint4 X;
-            if ((SC_GC & 2) && q + 16 <= n) {  // (the block's last 15 positions: from the LDS copy)
-              const auto v = __builtin_amdgcn_raw_buffer_load_b128(gb, (int)q, 0, 0);
-              X = make_uint4(v[0], v[1], v[2], v[3]);
-            } else {
-              X = sc_ld128(S.blk, q);
-            }
             const uint32_t p = q - off;
             if (SC_DUP & 4) sc_dup5(lds_addr(S.blk + (q & ~3u)));
             if (SC_DUP & 8) sc_dup5(lds_addr(S.blk + (p & ~3u)));
@@ -554,15 +586,9 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
               uint32_t x;
               asm volatile("ds_read_u16 %0, %1\ns_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(lds_addr(&Orow[i ^ osw2])) : "memory");
             }
-            uint32_t l;
-            if (SC_GC & 4) {
-              const auto v = __builtin_amdgcn_raw_buffer_load_b128(gb, (int)p, 0, 0);
-              const uint32_t b0 = sc_ffbl(X.x ^ v[0]), b1 = sc_ffbl(X.y ^ v[1]) | 32u;
-              const uint32_t b2 = sc_ffbl(X.z ^ v[2]) | 64u, b3 = sc_ffbl(X.w ^ v[3]) | 96u;
-              l = min(min(b0, b1), min(min(b2, b3), 128u)) >> 3;
-            } else {
-              l = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (p & ~3u)), p & 3u);
-            }
+            // the match length over 16 bytes: the first 4 are equal (the candidate check, C), so
+            // bytes [4, 16) of both sides decide it -- 12 bytes, three funnel-shifted dwords a side
+            const uint32_t l = 4u + sc_eq12(S.blk, q + 4, p + 4);
             const uint32_t avail = sce - q;
             enc = (l == 16 && avail > 16) ? kScExt : min(l, avail);
             Lrow[i ^ lsw4] = (uint8_t)enc;
@@ -1006,7 +1032,8 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
   }
   __syncthreads();
   // ---- the table as the in-order insert of positions [0, kScS k0) leaves it (section B's values:
-  // position + 1, group parity = slot; positions without 4 bytes before the block end never enter)
+  // positions, group parity = slot; positions without 4 bytes before the block end never enter;
+  // a never-written slot and position 0 both read 0, the same candidate)
   const uint32_t pe = (SC_SPAN_ABL & 1) ? 0u : kScS * k0;
   // (a lane takes four consecutive positions of one group -- two aligned dwords give their four
   // words -- and a wave four groups of the phase's parity per step)
@@ -1026,7 +1053,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
       if (ph) {
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
-          if (q + j + 4 <= n) __hip_atomic_fetch_max(t[j], (q + j + 1) << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (q + j + 4 <= n) __hip_atomic_fetch_max(t[j], (q + j) << 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {  // (the high half is final: only low halves change in this phase)
         uint32_t hi[4];
 #pragma unroll
@@ -1034,7 +1061,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j)
           if (q + j + 4 <= n)
-            __hip_atomic_fetch_max(t[j], (hi[j] & 0xffff0000u) | (q + j + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_max(t[j], (hi[j] & 0xffff0000u) | (q + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     __syncthreads();

@@ -17,6 +17,8 @@
 //   XSC=1      copies may run past the super-chunk end (to the block end)
 //   MERGE=1    literal runs merged across super-chunks
 //   SCS=n      super-chunk bytes (1024)
+//   HASH=1     the full-rate hash of round 5: ((w ^ (w >> 15)) * 0x9e3779 as u24 x u24) >> (32 - b)
+//   POS0=1     slots hold positions (not position + 1): an empty slot is candidate 0 (verified)
 // Prints per file: the model's size, the size the reference's parse gives (the oracle), the ratio.
 // Build: gcc -O2 -o /tmp/rm tools/ratio_model.c -L oracle -loracle_snappy -Wl,-rpath,$PWD/oracle
 // Run:   [FAR=256] /tmp/rm tests/golden/testdata/{alice29.txt,...}
@@ -30,6 +32,7 @@ static uint32_t ld32(const uint8_t* p) {
   memcpy(&v, p, 4);
   return v;
 }
+static int hashmode = 0, pos0 = 0;
 static int farmax = 1 << 30, blk = 65536, longnear = 0, margin = 0, tbits = 13, far_d = 256, longest = 0, long8 = 0, long16 = 0, xsc = 0, merge = 0, scs = 1024;
 
 static uint32_t lit_bytes(uint32_t n) { return n == 0 ? 0 : n + (n <= 60 ? 1 : (n <= 256 ? 2 : (n <= 65536 ? 3 : 4))); }
@@ -57,14 +60,21 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
     has[q] = 0;
     if (q + 4 > n) continue;
     const uint32_t w = ld32(b + q);
-    const uint32_t h = (w * 0x1e35a7bdu) >> (32 - tbits);
+    uint32_t h;
+    if (hashmode == 1) h = (((w ^ (w >> 15)) & 0xffffffu) * 0x9e3779u) >> (32 - tbits);
+    else if (hashmode == 2) h = ((w & 0xffffffu) * 0x9e3779u + (w >> 24) * 0x7a3c9bu) >> (32 - tbits);
+    else if (hashmode == 3) h = (((w & 0xffffffu) * 0x1e35a7u) ^ ((w >> 8) * 0x9e3779u)) >> (32 - tbits);
+    else if (hashmode == 4) h = ((w & 0xffffffu) * 0x1e35a7u + (w >> 8) * 0x2545f5u) >> (32 - tbits);
+    else if (hashmode == 5) h = (uint32_t)(((uint64_t)(w & 0xffffffu) * 0x9e3779u + (uint64_t)((w >> 8) & 0xffffffu) * 0x1e35a7u) >> 32) & ((1u << tbits) - 1);
+    else h = (w * 0x1e35a7bdu) >> (32 - tbits);
     const uint32_t par = (q >> 6) & 1;
     const uint32_t own = par ? T[h] >> 16 : T[h] & 0xffff, oth = par ? T[h] & 0xffff : T[h] >> 16;
-    T[h] = par ? (T[h] & 0xffff) | ((q + 1) << 16) : (T[h] & 0xffff0000u) | (q + 1);
+    const uint32_t qv = pos0 ? q : q + 1;
+    T[h] = par ? (T[h] & 0xffff) | (qv << 16) : (T[h] & 0xffff0000u) | qv;
     const uint32_t c1 = own > oth ? own : oth, c2 = own > oth ? oth : own;
-    const int m1 = c1 && ld32(b + c1 - 1) == w, m2 = c2 && ld32(b + c2 - 1) == w;
+    const uint32_t p1 = pos0 ? c1 : c1 - 1, p2 = pos0 ? c2 : c2 - 1;
+    const int m1 = (pos0 ? p1 < q : c1 != 0) && ld32(b + p1) == w, m2 = (pos0 ? p2 < q : c2 != 0) && ld32(b + p2) == w;
     if (!m1 && !m2) continue;
-    const uint32_t p1 = c1 - 1, p2 = c2 - 1;
     int use2 = m2 && (!m1 || (q - p1 < (uint32_t)far_d && q - p2 < (uint32_t)farmax));
     if (longnear && m1 && m2 && q - p1 < (uint32_t)far_d) {  // only a near recent one is compared
       const uint32_t lim = q + 16 < n ? q + 16 : n;
@@ -145,6 +155,8 @@ int main(int argc, char** argv) {
   if (getenv("XSC")) xsc = atoi(getenv("XSC"));
   if (getenv("MERGE")) merge = atoi(getenv("MERGE"));
   if (getenv("SCS")) scs = atoi(getenv("SCS"));
+  if (getenv("HASH")) hashmode = atoi(getenv("HASH"));
+  if (getenv("POS0")) pos0 = atoi(getenv("POS0"));
   double worst = 0, tot_m = 0, tot_r = 0;
   for (int f = 1; f < argc; ++f) {
     FILE* fp = fopen(argv[f], "rb");
