@@ -275,6 +275,14 @@ __device__ inline uint32_t sc_lit_tag(uint32_t len, uint32_t& sz) {
   return sz == 1 ? (l1 << 2) : (sz == 2 ? (60u << 2) | (l1 << 8) : (61u << 2) | (l1 << 8));
 }
 
+// the bucket of a word: the reference's multiply (internal.jl:94), its top kScTabBits bits, as one
+// v_bfe_u32 (the compiler's shift + mask + add of the bucket address is one VALU more)
+__device__ inline uint32_t sc_hash_bucket(uint32_t w) {
+  uint32_t h;
+  asm("v_bfe_u32 %0, %1, %2, %3" : "=v"(h) : "v"(w * kHashMul), "n"(32 - kScTabBits), "n"(kScTabBits));
+  return h;
+}
+
 // lane l: bit l of the lane mask m ? a : b (one v_cndmask on the SGPR pair)
 __device__ inline uint32_t sc_select(uint64_t m, uint32_t a, uint32_t b) {
   uint32_t r;
@@ -335,8 +343,9 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_eq16(uint32_t X0, u
 }
 
 
-// equal leading bytes (0..12) of the 12 bytes at x and at y of the LDS block copy
-__device__ __attribute__((always_inline)) inline uint32_t sc_eq12(const uint8_t* blk, uint32_t x, uint32_t y) {
+// 13 when the 12 bytes at x and at y of the LDS array blk are equal, else their equal leading
+// bytes (0..11): the walk's length code, 4 + this = 4..15 or kScExt (blk: 4-byte aligned)
+__device__ __attribute__((always_inline)) inline uint32_t sc_eq12x(const uint8_t* blk, uint32_t x, uint32_t y) {
   const uint32_t* a = reinterpret_cast<const uint32_t*>(blk + (x & ~3u));
   const uint32_t* b = reinterpret_cast<const uint32_t*>(blk + (y & ~3u));
   const uint32_t a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
@@ -344,7 +353,7 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_eq12(const uint8_t*
   const uint32_t f0 = sc_ffbl(sc_abyte(a1, a0, x) ^ sc_abyte(b1, b0, y));
   const uint32_t f1 = sc_ffbl(sc_abyte(a2, a1, x) ^ sc_abyte(b2, b1, y)) | 32u;
   const uint32_t f2 = sc_ffbl(sc_abyte(a3, a2, x) ^ sc_abyte(b3, b2, y)) | 64u;
-  return min(min(f0, f1), min(f2, 96u)) >> 3;
+  return min(min(f0, f1), min(f2, 104u)) >> 3;
 }
 
 // bits [a, b) of a u32 (0 <= a <= b <= 31)
@@ -396,7 +405,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     const uint32_t w = sc_abyte(sc_ld32(S.blk, qa + 64 * g + 4), sc_ld32(S.blk, qa + 64 * g), qb);
     if (SC_DUP & 64) sc_dup2(lds_addr(S.blk + qa + 64 * g));
     wq[g] = w;
-    ha[g] = Tbase + 4 * ((w * kHashMul) >> (32 - kScTabBits));
+    ha[g] = Tbase + 4 * sc_hash_bucket(w);
     hvv[g] = (g & 1) ? hv1 + ((64u * g) << 16) : hv0 + 64u * g;
   }
   if (sc0 + kScS + 3 > n) {  // (uniform) positions without 4 bytes exchange into the dummy word
@@ -558,48 +567,51 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   // the last token's extended length (one per lane: resync walks often end on the same token)
   uint32_t xpos = 16, xlen = 0;
   // Walk from row position sr (16: none) until the walk leaves the row or lands on a token of
-  // `stop`: the token bits, the merge position (16: none), the lane's end position.
-  auto walk = [&](uint32_t sr, uint32_t stop, uint32_t& path, uint32_t& mpos, uint32_t& pend) __attribute__((always_inline)) {
+  // `stop` (kStop; the first walk has none): the token bits, the merge position (16: none), the
+  // lane's end position.  A divergent loop: a lane leaves it when its walk ends (the next match
+  // position is past the row), so no values are carried through an exec-masked region; every
+  // iteration moves i forward by >= 4, so each lane leaves within 4 iterations.
+  auto walk = [&](auto kStop, uint32_t sr, uint32_t stop, uint32_t& path, uint32_t& mpos, uint32_t& pend)
+      __attribute__((always_inline)) {
     const uint32_t m0 = sr < 16 ? mask16 >> sr : 0u;
-    uint32_t i = m0 ? sr + (uint32_t)__builtin_ctz(m0) : 16u;
+    uint32_t i = sr + sc_ffbl(m0);  // (m0 == 0: no walk)
     path = 0;
     mpos = 16;
     uint32_t last = 16, lastL = 0;
-    bool act = i < 16;
-    while (ballot(act)) {
-      if (act) {
+    bool act = m0 != 0;
+    while (act) {
+      if constexpr (decltype(kStop)::value) {
         if ((stop >> i) & 1u) {
           mpos = i;
-          act = false;
-        } else {
-          path |= 1u << i;
-          last = i;
-          uint32_t enc;
-          if constexpr (kDense) {
-            enc = Lrow[i ^ lsw4];  // (computed in C)
-          } else {
-            const uint32_t q = c0 + i, off = offAt(i);
-            const uint32_t p = q - off;
-            if (SC_DUP & 4) sc_dup5(lds_addr(S.blk + (q & ~3u)));
-            if (SC_DUP & 8) sc_dup5(lds_addr(S.blk + (p & ~3u)));
-            if (SC_DUP & 16) {
-              uint32_t x;
-              asm volatile("ds_read_u16 %0, %1\ns_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(lds_addr(&Orow[i ^ osw2])) : "memory");
-            }
-            // the match length over 16 bytes: the first 4 are equal (the candidate check, C), so
-            // bytes [4, 16) of both sides decide it -- 12 bytes, three funnel-shifted dwords a side
-            const uint32_t l = 4u + sc_eq12(S.blk, q + 4, p + 4);
-            const uint32_t avail = sce - q;
-            enc = (l == 16 && avail > 16) ? kScExt : min(l, avail);
-            Lrow[i ^ lsw4] = (uint8_t)enc;
-          }
-          lastL = enc;
-          const uint32_t t = i + min(enc, 16u);  // <= 31: mask16 >> t is 0 past the row
-          const uint32_t m = mask16 >> t;
-          i = m ? t + (uint32_t)__builtin_ctz(m) : 16u;
-          act = i < 16;
+          break;
         }
       }
+      path |= 1u << i;
+      last = i;
+      uint32_t enc;
+      if constexpr (kDense) {
+        enc = Lrow[i ^ lsw4];  // (computed in C)
+      } else {
+        const uint32_t q = c0 + i, off = offAt(i);
+        const uint32_t p = q - off;
+        if (SC_DUP & 4) sc_dup5(lds_addr(S.blk + (q & ~3u)));
+        if (SC_DUP & 8) sc_dup5(lds_addr(S.blk + (p & ~3u)));
+        if (SC_DUP & 16) {
+          uint32_t x;
+          asm volatile("ds_read_u16 %0, %1\ns_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(lds_addr(&Orow[i ^ osw2])) : "memory");
+        }
+        // the match length over 16 bytes: the first 4 are equal (the candidate check, C), so bytes
+        // [4, 16) of both sides decide it: 4 + the equal leading bytes of 12, or kScExt (17) when
+        // all 12 are equal (the min's cap 104 >> 3 = 13); then capped at the super-chunk end
+        // (all 16 equal and more than 16 bytes left: kScExt, the walk's last token is extended)
+        enc = min(4u + sc_eq12x(S.blk + 4, q, p), sce - q);  // (blk + 4: the +4 in the loads' offsets)
+        Lrow[i ^ lsw4] = (uint8_t)enc;
+      }
+      lastL = enc;
+      const uint32_t t = i + min(enc, 16u);  // <= 31: mask16 >> t is 0 past the row
+      const uint32_t m = mask16 >> t;
+      i = t + sc_ffbl(m);
+      act = m != 0;
     }
     // the end: the last token's end when it leaves the row, else the row end (literals follow)
     pend = ce;
@@ -624,7 +636,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   uint32_t s = c0, e, P;
   {
     uint32_t mp;
-    walk(row ? 0u : 16u, 0u, P, mp, e);
+    walk(std::false_type{}, row ? 0u : 16u, 0u, P, mp, e);
     if (!row) e = c0;
   }
   for (; !(SC_ABL & 2);) {
@@ -635,7 +647,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     STAMP_COUNT(10, 1)
     const bool inrow = chg && sn < ce;  // (an entry is never before the row)
     uint32_t nP, mp, ne;
-    walk(inrow ? sn - c0 : 16u, P, nP, mp, ne);  // (rows not walking: stop at once)
+    walk(std::true_type{}, inrow ? sn - c0 : 16u, P, nP, mp, ne);  // (rows not walking: stop at once)
     if (chg) {
       s = sn;
       if (!inrow) {  // past the row (a copy jumped over it) or a lane without positions
