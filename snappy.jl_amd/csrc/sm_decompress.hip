@@ -110,8 +110,7 @@ __device__ inline uint32_t pack_sizes_slow(uint32_t cur, uint32_t nxt) {
 __device__ inline uint32_t pack_sizes(uint32_t cur, uint32_t nxt) {
   const uint32_t K = cur & 0x03030303u, H = (cur >> 2) & 0x3f3f3f3fu;
   const uint32_t csz = __builtin_amdgcn_perm(0u, 0x05030200u, K);       // kind 1/2/3 -> 2/3/5
-  const uint32_t nz = ((K + 0x7f7f7f7fu) & 0x80808080u) >> 7;          // 1 per copy byte
-  const uint32_t ml = (nz ^ 0x01010101u) * 0xffu;                       // 0xff per literal byte
+  const uint32_t ml = __builtin_amdgcn_perm(0u, 0x000000ffu, K);        // 0xff per literal byte (kind 0)
   const uint32_t sz = (csz & ~ml) | ((H + 0x02020202u) & ml);
   return ((H + 0x44444444u) & 0x80808080u & ml) ? pack_sizes_slow(cur, nxt) : sz;
 }
@@ -228,14 +227,20 @@ __device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t from
 __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt, uint32_t lane, uint32_t& cpos,
                                        uint32_t& csz, uint32_t& sizes) {
   sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
+  // (the rows hold byte offsets into a row, 2 x position: a read's address is the row base plus
+  // the value, no shift per read)
+  const uint8_t* const jb = reinterpret_cast<const uint8_t*>(jt);
+  auto rd = [&](int k, uint32_t x2) -> uint32_t {
+    return *reinterpret_cast<const uint16_t*>(jb + 2 * k * kJtRow + x2);
+  };
   uint32_t J[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint32_t p = 4 * lane + j;
     const uint32_t sz = (sizes >> (8 * j)) & 0xff;
-    J[j] = (sz == 255 || p >= rlim) ? p : min(p + sz, 256u);  // 256: beyond the window
+    J[j] = 2 * ((sz == 255 || p >= rlim) ? p : min(p + sz, 256u));  // 256: beyond the window
   }
-  if (lane < kWalkLevels) jt[lane * kJtRow + 256] = 256;  // every row maps 256 to itself
+  if (lane < kWalkLevels) jt[lane * kJtRow + 256] = 512;  // every row maps 256 to itself
   *reinterpret_cast<uint2*>(jt + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
   // The J_k are powers of J0, so they commute: lane t applies J_k for bit k of t as soon as row k
   // is built, its read issued with the next row's reads (the chain does not wait for every row)
@@ -243,23 +248,22 @@ __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt,
 #pragma unroll
   for (int k = 1; k < kWalkLevels; ++k) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const uint16_t* prev = jt + (k - 1) * kJtRow;
-    const uint32_t t = prev[c];
+    const uint32_t t = rd(k - 1, c);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) J[j] = prev[J[j]];
+    for (int j = 0; j < 4; ++j) J[j] = rd(k - 1, J[j]);
     c = ((lane >> (k - 1)) & 1u) ? t : c;
     *reinterpret_cast<uint2*>(jt + k * kJtRow + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
   }
   __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the u16 reads below follow the uint2 stores
   {
-    const uint32_t t = jt[(kWalkLevels - 1) * kJtRow + c];
+    const uint32_t t = rd(kWalkLevels - 1, c);
     c = ((lane >> (kWalkLevels - 1)) & 1u) ? t : c;
   }
   if (lane >= 32) {  // J5 = J4 o J4
-    const uint16_t* j4 = jt + (kWalkLevels - 1) * kJtRow;
-    c = j4[c];
-    c = j4[c];
+    c = rd(kWalkLevels - 1, c);
+    c = rd(kWalkLevels - 1, c);
   }
+  c >>= 1;  // (a position again)
   // (the shuffle runs with every lane active: a ds_bpermute from an inactive lane reads 0)
   const uint32_t szw = __shfl(sizes, (c >> 2) & 63u, 64);
   const uint32_t sz = c < 256 ? (szw >> (8 * (c & 3))) & 0xffu : 0u;

@@ -86,11 +86,22 @@ __host__ __device__ inline uint32_t hashtable_size(uint64_t n) {
 
 // internal.jl:35-46 layout: bits 0-7 length, 8-10 copy offset>>8, 11-13 extra bytes.
 __host__ __device__ inline uint32_t char_entry(uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // branch-free on the device: the kind-switch compiles to a divergent branch tree that a wave of
+  // mixed tags runs every arm of (exec masks, ~16 SALU); these are selects on the same values
+  const uint32_t kind = c & 3, hi = c >> 2;
+  const uint32_t tlc = __builtin_amdgcn_perm(0u, 0x04020100u, kind);  // copy tag bytes 1/2/4 (kind 0: 0)
+  const uint32_t lit = hi < 60 ? hi + 1 : (((hi - 59) << 11) | 1);
+  const uint32_t cp1 = (1u << 11) | ((c >> 5) << 8) | (4 + (hi & 7));
+  const uint32_t cpx = (tlc << 11) | (hi + 1);
+  return kind == 0 ? lit : (kind == 1 ? cp1 : cpx);
+#else
   uint32_t kind = c & 3, hi = c >> 2;
   if (kind == 0) return hi < 60 ? hi + 1 : (((hi - 59) << 11) | 1);
   if (kind == 1) return (1u << 11) | ((c >> 5) << 8) | (4 + ((c >> 2) & 7));
   if (kind == 2) return (2u << 11) | (hi + 1);
   return (4u << 11) | (hi + 1);
+#endif
 }
 
 __host__ __device__ inline uint32_t varint_len(uint32_t v) {
@@ -153,13 +164,13 @@ __device__ inline uint32_t scan_dpp(uint32_t v) {
 __device__ inline uint32_t lds_ld32(const uint8_t* lds, uint32_t pos) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (pos & ~3u));
   uint32_t lo = w[0], hi = w[1];
-  return __builtin_amdgcn_alignbyte(hi, lo, pos & 3u);
+  return __builtin_amdgcn_alignbyte(hi, lo, pos);  // (v_alignbyte_b32 shifts by 8 * S2[1:0]: no & 3)
 }
 
 // lds_ld64: >= 4 readable bytes past pos+7.
 __device__ inline uint64_t lds_ld64(const uint8_t* lds, uint32_t pos) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (pos & ~3u));
-  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = pos & 3u;
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], sh = pos;  // (alignbyte: S2[1:0] only)
   return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32) | __builtin_amdgcn_alignbyte(w1, w0, sh);
 }
 
