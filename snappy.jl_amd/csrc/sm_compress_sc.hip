@@ -492,7 +492,8 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     // bytes before the super-chunk end may not start a copy: the walks' row masks leave both out
     // (D), so no per-group check here.  (A candidate's loads read inside the block copy whatever
     // its value: c < 65536.)
-    const bool ok1 = c1 < q, ok2 = c2 < q;
+    // (c2 <= c1: when c1 is valid so is c2; when it is not -- the order broke -- both are dropped)
+    const bool ok1 = c1 < q;
     const uint32_t d1 = q - c1, d2 = q - c2;  // the offsets
     uint16_t* const Og = reinterpret_cast<uint16_t*>(Ob8 + (Orel ^ (4u * (g & 7))) + 128u * g);
     const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
@@ -503,7 +504,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       uint32_t lw1 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (c1 & ~3u)), c1);
       uint32_t lw2 = sc_eq16(X.x, X.y, X.z, X.w, reinterpret_cast<const uint32_t*>(S.blk + (c2 & ~3u)), c2);
       asm("" : "+v"(lw1), "+v"(lw2));  // (keeps the loads unconditional)
-      const uint32_t l1 = ok1 ? lw1 : 0u, l2 = ok2 ? lw2 : 0u;
+      const uint32_t l1 = ok1 ? lw1 : 0u, l2 = ok1 ? lw2 : 0u;
       const bool take2 = l2 == l1 ? (l2 >= 4 && d1 < (uint32_t)SC_FAR) : l2 > l1;
       const uint32_t l = take2 ? l2 : l1;
       const uint32_t avail = sce - q;  // (>= 4 where l >= 4: room)
@@ -528,7 +529,8 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       asm("" : "+v"(v1), "+v"(v2));  // (keeps the loads unconditional)
       // the matches as lane masks (ballots of plain compares, combined by SALU: a ballot of an
       // and-ed bool costs a v_cndmask + v_cmp, and a select on a combined bool two v_cndmask)
-      const uint64_t M1 = ballot(v1 == w) & ballot(ok1), M2 = ballot(v2 == w) & ballot(ok2);
+      const uint64_t OK = ballot(ok1);
+      const uint64_t M1 = ballot(v1 == w) & OK, M2 = ballot(v2 == w) & OK;
       // the older candidate when the more recent one is nearer than SC_FAR bytes: a copy whose
       // source is that close often reads the output of the decoder's own batch of tags, which
       // then runs it in order ("Candidates for the decoder")

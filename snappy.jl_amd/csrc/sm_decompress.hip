@@ -163,25 +163,35 @@ constexpr uint32_t kWin = SM_DEC_WIN;
 constexpr uint32_t kBatchOut = SM_DEC_BOUT;
 constexpr uint32_t kLdsSrc = kWin - kBatchOut - 64;
 
-// 8 bytes at byte x of an LDS ring of msk+1 bytes (power of 2, 8-aligned base): two aligned
-// ds_read_b64 and a funnel shift, the ring wrapping by index
-__device__ inline uint64_t lds_get8w(const uint8_t* bb, uint32_t msk, uint32_t x) {
-  const uint64_t* w = reinterpret_cast<const uint64_t*>(bb);
-  const uint32_t sl = x & msk, i = sl >> 3, sh = 8 * (sl & 7);
-  const uint64_t lo = w[i], hi = w[(i + 1) & (msk >> 3)];
-  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+// 8 bytes at byte x of an LDS ring of msk+1 bytes (power of 2, 4-aligned base) whose first 8
+// bytes are mirrored past its end: three aligned dword reads and two funnel shifts, no wrap, no
+// branch.  The input ring's mirror is written with its first slot (ring_put); the output window's
+// at the end of every batch (win_mirror): a round reads only bytes final before its batch.
+__device__ inline uint64_t lds_get8m(const uint8_t* bb, uint32_t msk, uint32_t x) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(bb + (x & msk & ~3u));
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
+  return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, x) << 32) | __builtin_amdgcn_alignbyte(w1, w0, x);
 }
 
-__device__ inline uint64_t win_get8(const uint8_t* win, uint32_t x) { return lds_get8w(win, kWin - 1, x); }
+__device__ inline uint64_t win_get8(const uint8_t* win, uint32_t x) { return lds_get8m(win, kWin - 1, x); }
 
-// OR the low cnt (1..8) bytes of v into the (zeroed) window at output position x
+// the window's first 8 bytes to its mirror (after every write of a batch; two lanes)
+__device__ inline void win_mirror(uint8_t* win, uint32_t lane) {
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  uint32_t* w = reinterpret_cast<uint32_t*>(win);
+  if (lane < 2) w[kWin / 4 + lane] = w[lane];
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
+// OR the low cnt (1..8) bytes of v into the (zeroed) window at output position x: two aligned
+// ds_or_b64, branch-free (the second ors 0 when nothing spills: (v >> 1) >> 63 is 0)
 __device__ inline void win_put8(uint8_t* win, uint32_t x, uint64_t v, uint32_t cnt) {
-  if (cnt < 8) v &= (1ull << (8 * cnt)) - 1;
+  v &= ~0ull >> (8 * (8 - cnt));  // (cnt >= 1: a shift of at most 56)
   uint64_t* w = reinterpret_cast<uint64_t*>(win);
   const uint32_t sl = x & (kWin - 1), i = sl >> 3, sh = 8 * (sl & 7);
   __hip_atomic_fetch_or(&w[i], v << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (sh && sh + 8 * cnt > 64)
-    __hip_atomic_fetch_or(&w[(i + 1) & (kWin / 8 - 1)], v >> (64 - sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __hip_atomic_fetch_or(&w[(i + 1) & (kWin / 8 - 1)], (v >> 1) >> (63 - sh), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // zero the window bytes of positions [x, x+len) (to the end of the last 8-byte word), keeping
@@ -295,6 +305,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   STAMP_DECL
   while ((int64_t)ip < Nm1 && op < op_lim) {
     STAMP_COUNT(6, 1)
+    win_mirror(win, lane);  // (the window's first 8 bytes as the previous batch or big literal left them)
     if (ip >= wb + 256) {
       if (__builtin_expect(ip < wb + 512, 1)) {
         ring_put(ring, wb + 768, pre1, lane);
@@ -428,13 +439,13 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
                 const uint32_t off = iscopy ? offset : 0xffffu;
                 // S's first 8 bytes, needed only when S wraps inside this pass (offset < base + 16)
                 uint64_t B = 0;
-                if (off < base + 8 * kPass) B = gsrc ? gload(slo) : lds_get8w(bb, msk, sp);
+                if (off < base + 8 * kPass) B = gsrc ? gload(slo) : lds_get8m(bb, msk, sp);
                 uint32_t m0 = base;
                 while (m0 >= off) m0 -= off;
                 uint32_t m = m0;
 #pragma unroll
                 for (int i = 0; i < kPass; ++i) {
-                  v[i] = base + 8 * i < L ? (gsrc ? gload(slo + m) : lds_get8w(bb, msk, sp + m))
+                  v[i] = base + 8 * i < L ? (gsrc ? gload(slo + m) : lds_get8m(bb, msk, sp + m))
                                           : 0ull;
                   m += 8;
                   if (m >= off) m -= off;
@@ -615,7 +626,7 @@ __device__ inline int32_t parse_header(const uint8_t* in, uint32_t N, uint32_t l
 __global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
   __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];  // tag-walk jump tables
-  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];                // output window
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin + 16];           // output window (+ mirror)
   const uint32_t lane = lane_id();
   const uint32_t b = blockIdx.x;
   const uint8_t* in = a.one_n ? a.in : a.in + a.in_off[b];
@@ -929,7 +940,7 @@ __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __res
                                                             uint8_t* out, const StreamFrag* frags, int32_t* status) {
   __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
   __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];
-  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin];
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin + 16];
   __shared__ __attribute__((aligned(16))) uint8_t sbuf[kIdxChunk + kIdxPad];
   const uint32_t f = blockIdx.x, lane = lane_id();
   const StreamFrag fr = frags[f];

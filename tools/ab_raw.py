@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--data", default="text")
     ap.add_argument("--mode", type=int, default=1)  # SM_MODE_FAST
+    ap.add_argument("--no-verify", action="store_true", help="ablation builds: their streams are not valid")
+    ap.add_argument("--compress-only", action="store_true")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -70,13 +72,15 @@ def main():
             comp(L, ctx)
             torch.cuda.synchronize()
             ratio = float(B.comp_len.to(torch.int64).sum()) / B.in_bytes
-            B.d_dec.fill_(0xAA)
-            unc(L, ctx)
-            torch.cuda.synchronize()
-            good = bool(torch.equal(B.d_dec, B.d_in)) and int(B.status.abs().sum()) == 0
-            ok &= good
+            good = False
+            if not a.no_verify:  # (an ablation's slots hold no valid streams: not decoded at all)
+                B.d_dec.fill_(0xAA)
+                unc(L, ctx)
+                torch.cuda.synchronize()
+                good = bool(torch.equal(B.d_dec, B.d_in)) and int(B.status.abs().sum()) == 0
+                ok &= good
             cm = bench.kernel_ms(lambda: comp(L, ctx), a.reps)
-            um = bench.kernel_ms(lambda: unc(L, ctx), a.reps)
+            um = 0.0 if (a.compress_only or a.no_verify) else bench.kernel_ms(lambda: unc(L, ctx), a.reps)
             res[name]["c"].append(cm)
             res[name]["u"].append(um)
             print("round %d %-28s compress %.4f ms  uncompress %.4f ms  ratio %.4f  roundtrip %s"

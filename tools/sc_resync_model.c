@@ -10,13 +10,14 @@
 static uint32_t ld32(const uint8_t* p){uint32_t v;memcpy(&v,p,4);return v;}
 static uint32_t T[8192], T2[8192], cand[65536];
 static long spec_lens, spec_iters;
-static int OV;
+static int OV, FIRST;
 static long n_sc, walk_iters1, rs_rounds, rs_iters, rs_lenlanes, rs_lanes_chg, first_lens, rs_lens, rs_rounds_needlen;
 static int lenAt(const uint8_t* d, uint32_t q, uint32_t sce, uint32_t* enc){
   uint32_t c=cand[q]; uint32_t l=0; while(l<16 && d[c+l]==d[q+l]) ++l;
   uint32_t av=sce-q; *enc = (l==16 && av>16)?17:(l<av?l:av); return 0;}
 int main(int argc,char**argv){
   if(getenv("OV")) OV=atoi(getenv("OV"));
+  if(getenv("FIRST")) FIRST=atoi(getenv("FIRST"));  // the first walk from row position FIRST (lane 0: 0)
   for(int f=1;f<argc;++f){FILE*fp=fopen(argv[f],"rb");fseek(fp,0,SEEK_END);long sz=ftell(fp);fseek(fp,0,SEEK_SET);
   uint8_t*d=calloc(sz+64,1);if(fread(d,1,sz,fp)!=(size_t)sz) return 2;fclose(fp);
   for(long o=0;o<sz;o+=65536){uint32_t n=sz-o<65536?sz-o:65536; const uint8_t*b=d+o;
@@ -39,7 +40,7 @@ int main(int argc,char**argv){
           uint32_t t=i+(enc<16?enc:16); uint32_t m=mask[l]>>t; i=m?t+__builtin_ctz(m):16; } \
         pend=ce; if(last<16){uint32_t L=lastL; if(last+(L<16?L:16)>=16){ if(L==17){uint32_t q=c0+last,c=cand[q];L=16;uint32_t cap=sce-q<255?sce-q:255;while(L<cap&&b[c+L]==b[q+L])++L;} pend=c0+last+L;}} }
       int mx=0, mx0=0;
-      for(int l=0;l<64;++l){uint32_t c0=sc0+16*l; uint32_t mp,st; uint32_t s0=c0, st0=0;
+      for(int l=0;l<64;++l){uint32_t c0=sc0+16*l; uint32_t mp,st; uint32_t s0=c0+(l?FIRST:0), st0=0;
         if(OV && l>0 && c0<sce){  // speculative entry: walk the previous row from OV bytes before
           uint32_t pr=l-1, pc0=sc0+16*pr; uint32_t i=16-OV; uint32_t m0=mask[pr]>>i; i=m0?i+__builtin_ctz(m0):16;
           uint32_t pos=pc0+i;
