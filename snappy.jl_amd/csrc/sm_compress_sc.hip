@@ -50,8 +50,19 @@ constexpr uint32_t kScC = kScS / 64;      // positions per lane (16)
 constexpr uint32_t kScG = kScS / 64;      // 64-position groups per super-chunk (16)
 constexpr uint32_t kScW = 16;             // waves per workgroup: kScW - 1 workers and the writer
 constexpr uint32_t kScWorkers = kScW - 1;
-constexpr uint32_t kScRing = 8;           // staging slots between the workers and the writer
-constexpr uint32_t kScSlot = 1280;        // bytes per slot (a super-chunk's output is at most ~1.1 KiB)
+#ifndef SC_RING
+#define SC_RING 16
+#endif
+// staging slots between the workers and the writer: one per worker and one more, so a worker that
+// finishes its super-chunk stages it at once (with 8 slots, the workers 8 or more super-chunks ahead
+// of the writer waited for one: half of their wave time in the section stamps, tools/sc_stamps.py)
+constexpr uint32_t kScRing = SC_RING;
+static_assert((kScRing & (kScRing - 1)) == 0, "the span kernel's slot sequence needs a power of 2");
+// bytes per slot: a super-chunk's output is at most 1,040 bytes (1,024 input bytes; every copy tag
+// is shorter than its copy, every maximal literal run adds a 1-byte tag, 2 or 3 bytes only for runs
+// over 60 bytes, of which at most 15 fit between copies), plus the 20-byte reach of the last piece's
+// or and the writer's one-unit read-ahead
+constexpr uint32_t kScSlot = 1088;
 constexpr uint32_t kScThreads = 64 * kScW;
 constexpr uint32_t kScTabBits = 13;       // 8 K dword buckets of two u16 slots
 constexpr uint32_t kScTabWords = 1u << kScTabBits;

@@ -113,7 +113,7 @@ hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t*
 // bytes as the whole-block parse).  Part j of block b writes at out + out_off[b] + j pitch (pitch >=
 // span kSpanSlot) and its length to part_len[b parts + j]; parts * span >= 64.  Runs the screen
 // first.
-constexpr uint32_t kSpanSlot = 1280;  // a super-chunk's output bound (k_compress_sc's staging slot)
+constexpr uint32_t kSpanSlot = 1088;  // a super-chunk's output bound (k_compress_sc's staging slot)
 struct ScSpan {
   uint32_t parts, span;
   uint64_t pitch;

@@ -245,6 +245,32 @@ def test_fast_mode_batched_roundtrip(sm, oracle, libsnappy, gpu_available, corpu
     assert ratio < ref * 1.10, (ratio, ref)   # fast parse stays within 10% of the reference size
 
 
+@pytest.mark.parametrize("mode", FAST_MODES)
+def test_fast_mode_largest_superchunk_outputs(sm, oracle, gpu_available, mode):
+    """Blocks whose 1 KiB super-chunks come out as large as they can (k_compress_sc's staging
+    slot holds 1,088 bytes; the bound is 1,040): literal runs of 61-64 bytes, each with a 2-byte
+    tag, between short copies from more than 2 KiB back (3-byte tags), at every phase of the
+    super-chunk grid, and runs that straddle lanes and super-chunks.  Every stream decodes under
+    the oracle and is at most one literal of its block."""
+    rng = np.random.default_rng(0x5107)
+    base = rng.integers(0, 256, 4096, dtype=np.uint8).tobytes()
+    blocks = []
+    for run in (61, 62, 64, 60, 59):
+        for phase in (0, 1, 7, 333):
+            parts = [base, rng.integers(0, 256, phase, dtype=np.uint8).tobytes()]
+            n = sum(map(len, parts))
+            while n < 65536:
+                lit = rng.integers(0, 256, run, dtype=np.uint8).tobytes()
+                src = int(rng.integers(0, 4096 - 8))
+                parts += [lit, base[src:src + 4]]
+                n += run + 4
+            blocks.append(b"".join(parts)[:65536])
+    outs = sm.compress_batch(blocks, mode=mode)
+    for blk, out in zip(blocks, outs):
+        assert oracle.uncompress(out) == blk
+        assert len(out) <= 3 + 3 + len(blk)
+
+
 # ---- decompress -------------------------------------------------------------------------
 
 def test_decompress_corpus_and_golden(sm, oracle, libsnappy, gpu_available, corpus):
