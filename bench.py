@@ -49,7 +49,7 @@ BLOCK = 65536
 SLOT = 76496  # >= max_compressed_length(65536) = 76490, 16-B aligned
 HBM_PEAK_GBPS = 8000.0
 METRIC = "GB/s compressed+decompressed (batched blocks) at 1/2/4/8 GPUs; % HBM peak"  # BASELINE.json
-ROUND = "r04"
+ROUND = "r05"
 
 # test/runtests.jl:8-24, the round-trip corpus; config 5 tiles it
 ROUNDTRIP_FILES = ["alice29.txt", "asyoulik.txt", "html", "html_x_4", "kppkn.gtb", "lcet10.txt", "fireworks.jpeg",
@@ -293,11 +293,23 @@ def kernel_ms(fn, reps):
 
 
 def pmc_traffic(kernel):
-    path = os.path.join(ROOT, "profiles", ROUND + "_pmc.json")
+    """HBM bytes per launch from the round's PMC file (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, run
+    separately from this process: counters cannot be collected inside a timed run), with where
+    they came from: the file, the library build and commit the passes measured, and whether that
+    build is the one this run loaded (a stale file is labelled, never silently reported)."""
+    rel = os.path.join("profiles", ROUND + "_pmc.json")
     try:
-        return json.load(open(path)).get(kernel, {}).get("hbm_bytes_per_launch")
+        d = json.load(open(os.path.join(ROOT, rel)))
     except Exception:
-        return None
+        return None, {"file": rel, "present": False}
+    lib = d.get("library")
+    try:
+        cur = load_package_cached().version()
+    except Exception:
+        cur = None
+    src = {"file": rel, "library": lib, "commit": d.get("commit"), "this_run_library": cur,
+           "same_build": bool(lib) and lib == cur}
+    return d.get(kernel, {}).get("hbm_bytes_per_launch"), src
 
 
 # the rocprof kernels behind each timed call (a fast-mode compress is the incompressible screen
@@ -313,9 +325,10 @@ ROCPROF_KERNELS = {
 
 def roofline(kernel, alg_bytes, ms):
     achieved = alg_bytes / (ms * 1e-3) / 1e9
+    traffic, src = pmc_traffic(kernel)
     return {"kernel": kernel, "rocprof_kernels": ROCPROF_KERNELS.get(kernel), "bound": "hbm",
             "achieved": round(achieved, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": pmc_traffic(kernel),
+            "frac": round(achieved / HBM_PEAK_GBPS, 5), "traffic": traffic, "traffic_source": src,
             "algorithmic_bytes_per_launch": int(alg_bytes), "avg_launch_ms": round(ms, 4)}
 
 

@@ -324,14 +324,14 @@ __device__ inline uint32_t sc_extend(const uint8_t* blk, uint32_t q, uint32_t of
   }
 }
 
-// copy_tag_bytes (emit_copy!, internal.jl:306-329) for 4 <= L <= 255 in closed form: k 64-byte
-// pieces while L >= 68, a 60-byte piece if more than 64 remain, then one piece of <= 64
+// copy_tag_bytes (emit_copy!, internal.jl:306-329) for 4 <= L <= 255 in closed form.  emit_copy!
+// cuts 64-byte pieces while L >= 68, a 60-byte piece if more than 64 remain, then the last piece R:
+// (L - 1) >> 6 three-byte pieces before the last, and R < 12 exactly when ((L - 1) & 63) < 11
+// (R = m + 4 for m = ((L - 1) & 63) + 1 < 4, else m) -- checked for every L and both offset
+// classes against the loop (tests/test_host_logic.py); no multiply (3 n as n + 2 n)
 __device__ inline uint32_t sc_copy_bytes(uint32_t off, uint32_t L) {
-  const uint32_t k = L >= 68 ? (L - 4) >> 6 : 0u;
-  const uint32_t R0 = L - 64 * k;
-  const uint32_t x = R0 > 64 ? 1u : 0u;
-  const uint32_t R = R0 - 60 * x;
-  return 3 * (k + x) + ((R < 12 && off < 2048) ? 2u : 3u);
+  const uint32_t t = L - 1, n = t >> 6;
+  return n + 2 * n + (((t & 63) < 11 && off < 2048) ? 2u : 3u);
 }
 
 // lowest set bit of x, ~0 for 0 (v_ffbl_b32)

@@ -69,3 +69,24 @@ def test_bench_visible_gpus_from_sysfs(monkeypatch):
     monkeypatch.setitem(sys.modules, "torch", fake)
     args = types.SimpleNamespace(gpus=2)
     assert bench.launch_ranks(args) == 2
+
+
+def test_copy_tag_bytes_closed_form():
+    """k_compress_sc's sc_copy_bytes: emit_copy!'s tag bytes (src/internal.jl:306-329) in closed
+    form, 3 ((L - 1) >> 6) + (2 if ((L - 1) & 63) < 11 and offset < 2048 else 3), against the
+    reference's piece loop for every copy length the kernel emits (4..255) and both offset classes."""
+    def loop(off, L):
+        b = 0
+        while L >= 68:
+            b, L = b + 3, L - 64
+        if L > 64:
+            b, L = b + 3, L - 60
+        return b + (2 if (L < 12 and off < 2048) else 3)
+
+    def closed(off, L):
+        t = L - 1
+        return 3 * (t >> 6) + (2 if ((t & 63) < 11 and off < 2048) else 3)
+
+    for off in (1, 7, 2047, 2048, 30000, 65535):
+        for L in range(4, 256):
+            assert closed(off, L) == loop(off, L), (off, L)

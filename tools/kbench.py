@@ -24,6 +24,9 @@ def main():
     args = ap.parse_args()
     sm = bench.load_package()
     dev = torch.device("cuda", 0)
+    print("library", sm.version())
+    if args.op in ("compress_fragments", "uncompress_fragments"):
+        return fragments(sm, dev, args)
     blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 0x5EED + 1)
     b = bench.Batch(blocks, dev)
     b.compress(sm, "fast")
@@ -48,6 +51,25 @@ def main():
     if args.op != "uncompress":
         b.uncompress(sm)
     print("roundtrip ok:", b.verify())
+
+
+def fragments(sm, dev, args):
+    """Config 5 (bench.py `large`): the 644 MiB stream's 10,304 fragments on one GPU."""
+    big = bench.large_corpus()
+    nfrag = (big.size + bench.BLOCK - 1) // bench.BLOCK
+    sh = bench.StreamShard(big, 0, nfrag, dev)
+    sh.compress(sm)
+    torch.cuda.synchronize()
+    fn = (lambda: sh.compress(sm)) if args.op == "compress_fragments" else (lambda: sh.uncompress(sm))
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.reps):
+        fn()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.reps
+    print("%s: %.3f ms/launch, %.2f GB/s (uncompressed bytes)" % (args.op, dt * 1e3, sh.in_bytes / dt / 1e9))
+    print("roundtrip ok:", sh.verify(sm))
 
 
 if __name__ == "__main__":

@@ -23,5 +23,6 @@ bash tools/pmc_run.sh compress_fast "$OUT/pmc_compress" text || exit 1
 bash tools/pmc_run.sh uncompress "$OUT/pmc_uncompress" text || exit 1
 bash tools/pmc_run.sh compress_fast "$OUT/pmc_compress_random" random || exit 1
 bash tools/pmc_run.sh uncompress "$OUT/pmc_uncompress_random" random || exit 1
-python3 tools/pmc_json.py "$OUT" "$OUT/pmc.json"
+bash tools/pmc_run.sh compress_fragments "$OUT/pmc_compress_fragments" text || exit 1
+python3 tools/pmc_json.py "$OUT" "$OUT/pmc.json" "${COMMIT:-}"
 echo profile done
