@@ -99,6 +99,9 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #ifndef SC_GC
 #define SC_GC 0
 #endif
+#ifndef SC_CB  // fast mode: section C's groups per batch of candidate loads in flight
+#define SC_CB 2
+#endif
 #ifndef SC_FAR  // fast mode: the older of two matching candidates when the recent one is nearer
 #define SC_FAR 256
 #endif
@@ -489,26 +492,25 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   // unswizzled offset in group 0 (bits 2..4 are 2 i's) -- one XOR a group, 128 g an immediate offset
   uint8_t* const Ob8 = reinterpret_cast<uint8_t*>(Wl.O);
   const uint32_t Orel = 32 * (lane >> 4) + 2 * (lane & 15);
+  // A candidate is valid when it is an earlier position: c < q.  The table is cleared per block and
+  // filled in position order, so every slot value is an earlier position whenever the conflicting
+  // lanes of one ds_mskor_rtn are serviced in ascending lane order (observed on gfx950); the compare
+  // makes validity independent of that order.  c2 <= c1: when c1 is valid so is
+  // c2; when it is not -- the order broke -- both are dropped.  Positions without 4 bytes before the
+  // block end exchanged with the dummy word, and positions without 4 bytes before the super-chunk
+  // end may not start a copy: the walks' row masks leave both out (D), so no per-group check here.
+  // (A candidate's loads read inside the block copy whatever its value: c < 65536.)
+  if constexpr (kDense) {
 #pragma unroll
-  for (int g = 0; g < (int)kScG; ++g) {
-    const uint32_t q = sc0 + 64 * g + lane;
-    const uint32_t sh = 16 * (g & 1);
-    const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // positions
-    const uint32_t c1 = (SC_ABL & 8) ? q : max(ca, cb), c2 = (SC_ABL & 8) ? q : min(ca, cb);
-    // A candidate is valid when it is an earlier position: c < q.  The table is cleared per block
-    // and filled in position order, so every slot value is an earlier position whenever the
-    // conflicting lanes of one ds_mskor_rtn are serviced in ascending lane order (observed on
-    // gfx950); the compare makes validity independent of that order.  Positions
-    // without 4 bytes before the block end exchanged with the dummy word, and positions without 4
-    // bytes before the super-chunk end may not start a copy: the walks' row masks leave both out
-    // (D), so no per-group check here.  (A candidate's loads read inside the block copy whatever
-    // its value: c < 65536.)
-    // (c2 <= c1: when c1 is valid so is c2; when it is not -- the order broke -- both are dropped)
-    const bool ok1 = c1 < q;
-    const uint32_t d1 = q - c1, d2 = q - c2;  // the offsets
-    uint16_t* const Og = reinterpret_cast<uint16_t*>(Ob8 + (Orel ^ (4u * (g & 7))) + 128u * g);
-    const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
-    if constexpr (kDense) {
+    for (int g = 0; g < (int)kScG; ++g) {
+      const uint32_t q = sc0 + 64 * g + lane;
+      const uint32_t sh = 16 * (g & 1);
+      const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // positions
+      const uint32_t c1 = (SC_ABL & 8) ? q : max(ca, cb), c2 = (SC_ABL & 8) ? q : min(ca, cb);
+      const bool ok1 = c1 < q;
+      const uint32_t d1 = q - c1, d2 = q - c2;  // the offsets
+      uint16_t* const Og = reinterpret_cast<uint16_t*>(Ob8 + (Orel ^ (4u * (g & 7))) + 128u * g);
+      const uint32_t r4 = 4 * g + (lane >> 4), i = lane & 15;  // row, entry
       // dense mode: both candidates compared over 16 bytes, the longer kept, its length stored
       // for the walks; on a tie the SC_FAR rule below (the older when the more recent is near)
       const uint4 X = sc_ld128(S.blk, q);
@@ -523,31 +525,53 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       *Og = (uint16_t)(take2 ? d2 : d1);
       Wl.L[16 * r4 + 4 * ((i >> 2) ^ ((g >> 1) & 3)) + (i & 3)] = (uint8_t)enc;
       mbs[g] = ballot(l >= 4);
-    } else {
-      uint32_t v1, v2;
-      if (SC_GC & 1) {
-        v1 = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)c1, 0, 0);
-        v2 = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)c2, 0, 0);
-      } else {
-        v1 = sc_ld32u(S.blk, c1);
-        v2 = sc_ld32u(S.blk, c2);
+    }
+  } else {
+    // fast mode: SC_CB groups at a time, all their candidate loads issued before any is waited for
+#pragma unroll
+    for (int g0 = 0; g0 < (int)kScG; g0 += SC_CB) {
+      uint32_t c1s[SC_CB], c2s[SC_CB], v1s[SC_CB], v2s[SC_CB];
+#pragma unroll
+      for (int j = 0; j < SC_CB; ++j) {
+        const int g = g0 + j;
+        const uint32_t q = sc0 + 64 * g + lane;
+        const uint32_t sh = 16 * (g & 1);
+        const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // positions
+        c1s[j] = (SC_ABL & 8) ? q : max(ca, cb);
+        c2s[j] = (SC_ABL & 8) ? q : min(ca, cb);
+        if (SC_GC & 1) {
+          v1s[j] = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)c1s[j], 0, 0);
+          v2s[j] = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)c2s[j], 0, 0);
+        } else {
+          v1s[j] = sc_ld32u(S.blk, c1s[j]);
+          v2s[j] = sc_ld32u(S.blk, c2s[j]);
+        }
+        if (SC_DUP & 2) {
+          sc_dup2(lds_addr(S.blk + (c1s[j] & ~3u)));
+          sc_dup2(lds_addr(S.blk + (c2s[j] & ~3u)));
+        }
       }
-      if (SC_DUP & 2) {
-        sc_dup2(lds_addr(S.blk + (c1 & ~3u)));
-        sc_dup2(lds_addr(S.blk + (c2 & ~3u)));
+#pragma unroll
+      for (int j = 0; j < SC_CB; ++j) asm("" : "+v"(v1s[j]), "+v"(v2s[j]));  // (keeps the loads unconditional)
+#pragma unroll
+      for (int j = 0; j < SC_CB; ++j) {
+        const int g = g0 + j;
+        const uint32_t q = sc0 + 64 * g + lane;
+        const uint32_t c1 = c1s[j], c2 = c2s[j], w = wq[g];
+        const bool ok1 = c1 < q;
+        const uint32_t d1 = q - c1, d2 = q - c2;  // the offsets
+        uint16_t* const Og = reinterpret_cast<uint16_t*>(Ob8 + (Orel ^ (4u * (g & 7))) + 128u * g);
+        // the matches as lane masks (ballots of plain compares, combined by SALU: a ballot of an
+        // and-ed bool costs a v_cndmask + v_cmp, and a select on a combined bool two v_cndmask)
+        const uint64_t OK = ballot(ok1);
+        const uint64_t M1 = ballot(v1s[j] == w) & OK, M2 = ballot(v2s[j] == w) & OK;
+        // the older candidate when the more recent one is nearer than SC_FAR bytes: a copy whose
+        // source is that close often reads the output of the decoder's own batch of tags, which
+        // then runs it in order ("Candidates for the decoder")
+        const uint64_t U = M2 & (~M1 | ballot(d1 < (uint32_t)SC_FAR));
+        *Og = (uint16_t)sc_select(U, d2, d1);  // (a position without a match: never read)
+        mbs[g] = M1 | M2;
       }
-      const uint32_t w = wq[g];
-      asm("" : "+v"(v1), "+v"(v2));  // (keeps the loads unconditional)
-      // the matches as lane masks (ballots of plain compares, combined by SALU: a ballot of an
-      // and-ed bool costs a v_cndmask + v_cmp, and a select on a combined bool two v_cndmask)
-      const uint64_t OK = ballot(ok1);
-      const uint64_t M1 = ballot(v1 == w) & OK, M2 = ballot(v2 == w) & OK;
-      // the older candidate when the more recent one is nearer than SC_FAR bytes: a copy whose
-      // source is that close often reads the output of the decoder's own batch of tags, which
-      // then runs it in order ("Candidates for the decoder")
-      const uint64_t U = M2 & (~M1 | ballot(d1 < (uint32_t)SC_FAR));
-      *Og = (uint16_t)sc_select(U, d2, d1);  // (a position without a match: never read)
-      mbs[g] = M1 | M2;
     }
   }
   // the row masks: lane d holds dword d of the 16 group ballots (v_writelane), lane l reads its
