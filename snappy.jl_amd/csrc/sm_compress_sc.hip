@@ -246,6 +246,18 @@ __device__ inline uint4 sc_trim(uint4 v, uint32_t len) {
   return make_uint4(v.x & (uint32_t)mlo, v.y & (uint32_t)(mlo >> 32), v.z & (uint32_t)mhi, v.w & (uint32_t)(mhi >> 32));
 }
 
+// v with the bytes from len (1..16) on cleared, by two 64-bit right shifts of all-ones (the shift
+// amounts stay in 0..56 for len >= 1; the high half is dropped by a select when len <= 8)
+__device__ inline uint4 sc_trim1(uint4 v, uint32_t len) {
+  uint32_t l8 = len << 3;
+  asm("" : "+v"(l8));  // (else the compiler folds 128 - 8 len into a quarter-rate multiply by 56)
+  const uint64_t mlo = ~0ull >> (64 - min(l8, 64u));
+  const uint64_t mhi = ~0ull >> (128 - l8);  // (v_lshrrev_b64 reads 6 bits; len > 8: 0..56)
+  const bool hi = len > 8;
+  return make_uint4(v.x & (uint32_t)mlo, v.y & (uint32_t)(mlo >> 32), hi ? v.z & (uint32_t)mhi : 0u,
+                    hi ? v.w & (uint32_t)(mhi >> 32) : 0u);
+}
+
 // ors the 16 bytes v (zero past the piece) into the zeroed LDS byte array at byte address a (any
 // alignment): five ds_or_b32, unconditionally (an or of zeros leaves a neighbour's bytes alone)
 __device__ inline void sc_lds_or(uint32_t a, uint4 v) {
@@ -788,7 +800,8 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
           // onto itself one byte early -- no prepend shifts
           uint4 v = sc_ld128(S.blk - 4, p + 3);  // bytes from position p - 1
           v.x = ts ? ((v.x & ~0xffu) | ((run - 1) << 2)) : v.x;
-          sc_lds_or(stga + at + ts - 1u, sc_trim(v, run ? run + 1 : 0u));
+          // (lanes without a run write nothing: a shared dummy address serialises the atomics)
+          if (run) sc_lds_or(stga + at + ts - 1u, sc_trim1(v, run + 1));
         }
         at += len;
         if (L <= 64) {

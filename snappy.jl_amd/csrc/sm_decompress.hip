@@ -32,7 +32,7 @@
 #include "sm_device.h"
 #include "sm_internal.h"
 
-#ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only), 4 = no HBM sources (timing only)
+#ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only), 4 = no HBM sources, 8 = no fence before HBM sources (timing only)
 #define SM_ABLATE_D 0
 #endif
 
@@ -391,7 +391,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const bool longlit = !iscopy && litlen > 64;
       uint64_t done = (ballot(longlit) & all) | ~all;
       // HBM sources: this wave's earlier flushes (and big literals) must have landed
-      if (ballot(act_t && gsrc)) __threadfence_block();
+      if (!(SM_ABLATE_D & 8) && ballot(act_t && gsrc)) __threadfence_block();
 
       // long literals (65..200 B, no dependencies, inside the input ring): whole-wave passes
       uint64_t lm = ballot(act_t && longlit);

@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--mode", type=int, default=1)  # SM_MODE_FAST
     ap.add_argument("--no-verify", action="store_true", help="ablation builds: their streams are not valid")
     ap.add_argument("--compress-only", action="store_true")
+    ap.add_argument("--decode-ablation", action="store_true",
+                    help="the first build compresses once; every build's uncompress of those streams is timed, "
+                         "unverified (decoder ablation builds)")
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -66,6 +69,17 @@ def main():
         assert st == 0, st
 
     res = {name: {"c": [], "u": []} for name, _, _ in libs}
+    if a.decode_ablation:
+        comp(libs[0][1], libs[0][2])
+        torch.cuda.synchronize()
+        for r in range(a.rounds):
+            for name, L, ctx in libs:
+                um = bench.kernel_ms(lambda: unc(L, ctx), a.reps)
+                res[name]["u"].append(um)
+                print("round %d %-28s uncompress %.4f ms" % (r, name, um), flush=True)
+        for name, v in res.items():
+            print("%-28s uncompress min %.4f med %.4f" % (name, min(v["u"]), float(np.median(v["u"]))))
+        return
     ok = True
     for r in range(a.rounds):
         for name, L, ctx in libs:
