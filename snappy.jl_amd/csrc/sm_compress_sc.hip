@@ -175,9 +175,6 @@ __device__ inline void sc_dup2(uint32_t wa) {
 
 __device__ inline uint32_t sc_ld32(const uint8_t* blk, uint32_t a) { return *reinterpret_cast<const uint32_t*>(blk + a); }
 
-__device__ inline uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
 
 // (v_alignbyte_b32 shifts by 8 * S2[1:0]: the shift operands below are byte addresses, unmasked --
 // a `& 3` costs a VALU the compiler does not drop)

@@ -10,23 +10,17 @@
 // The first error in stream order wins, as the reference throws at the first one.
 //
 // Batched tag engine (declared length <= 64 KiB -- every block the compressor produces):
-//  * output written straight to HBM (the block's output region), so a wave needs only its
-//    1 KiB LDS ring and occupancy is set by VGPRs (many blocks in flight per CU hide the
-//    store->load latency of copies); a workgroup-scope fence (s_waitcnt) orders a round's
-//    copy-source loads after the earlier rounds' stores of the same wave;
-//  * the compressed stream flows through a 1 KiB LDS ring (4 x 256-B slots + 16-B mirror),
-//    one slot prefetched into registers a batch ahead;
+//  * the compressed stream flows through a 1 KiB LDS ring (4 x 256-B slots + mirror), one
+//    slot prefetched into registers a batch ahead;
 //  * every lane computes, for its 4 positions of the current slot, the size a tag starting
-//    there would have (packed u8, 255 = literal too long for a batch), so the serial tag walk
-//    is one v_readlane + a few SALU ops per tag;
-//  * up to 64 tags per batch decode one per lane (unaligned ds_read_b64 of the ring), output
-//    offsets from a wave scan, the reference's error checks per tag -- the lowest failing lane
-//    decides the status;
-//  * tags execute lane-parallel in 8-byte chunks (unaligned global dwordx2 loads/stores), in
-//    dependency rounds: a copy runs once every earlier tag of the batch its source overlaps
-//    has run.  Overlapping copies (offset < 8) first build the 8-byte period pattern, then
-//    advance with an effective offset that is a multiple of the period -- exactly the bytes
-//    incremental_copy_slow! (internal.jl:477-481) produces.
+//    there would have (packed u8, 255 = literal too long for a batch); a pointer-doubling walk
+//    gives lane t the t-th tag directly;
+//  * up to 64 tags per batch decode one per lane, output offsets from a wave scan, the
+//    reference's error checks per tag -- the lowest failing lane decides the status;
+//  * tags execute lane-parallel in 16-byte pieces into a linear LDS output window (sources in
+//    the window or, older, in HBM), the few copies whose source overlaps the batch's own
+//    output (or offset < 16) in stream order after them; whole 16-byte blocks go to HBM when
+//    a batch ends.
 // Literals longer than 64 bytes are copied by the whole wave.
 // Streams declaring > 64 KiB use a simple per-tag engine (also straight into HBM).
 #include "sm_device.h"
@@ -34,6 +28,14 @@
 
 #ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only), 4 = no HBM sources, 8 = no fence before HBM sources (timing only)
 #define SM_ABLATE_D 0
+#endif
+
+#ifndef SM_DUP_D  // diagnostic builds only: sections run twice (1 walk, 2 decode, 4 flush, 8 execution round) for their instruction counts
+#define SM_DUP_D 0
+#endif
+
+#ifndef SM_DEC_QUEUE  // diagnostic builds only: 1 = persistent waves on a global stream queue (k_decompress_q), 2 = also check the grab
+#define SM_DEC_QUEUE 0
 #endif
 
 #ifndef SM_IDX_NOLANES
@@ -51,24 +53,13 @@ typedef uint16_t __attribute__((aligned(1))) du16u;
 typedef uint32_t __attribute__((aligned(1))) du32u;
 typedef uint64_t __attribute__((aligned(1))) du64u;
 
-// 8 bytes of earlier output at p for a far copy source (its destination starts at lim >= p + 1,
-// lim >= 8): the load never reaches lim -- the stream (and the caller's buffer) may end a few
-// bytes after it -- and the bytes at or past lim, which the copy masks off anyway, read as 0.
-__device__ inline uint64_t out_get8(const uint8_t* out, uint32_t p, uint32_t lim) {
-  const uint32_t a = min(p, lim - 8);
-  return *reinterpret_cast<const du64u*>(out + a) >> (8 * (p - a));
-}
-
 constexpr uint32_t kRing = 1024;
+constexpr uint32_t kRingMirror = 96;  // the ring's first bytes again past its end: a literal's
+                                      // 16-byte pieces (<= 64 B) read at ring offset + 48 + 20
 constexpr uint32_t kMaxBatchLit = 200;  // longer literals stop a window walk (size 255)
 constexpr int kWalkLevels = 5;  // tables J0..J4 in LDS; J5 (bit 5 of a lane's chain index) = J4 o J4
 constexpr int kJtRow = 264;             // a jump-table row (u16): positions 0..255, then 256 = beyond the window
 constexpr int kJt = kWalkLevels * kJtRow;  // u16 jump-table entries of a walk
-#ifndef SM_DEC_PASS
-#define SM_DEC_PASS 2
-#endif
-constexpr int kPass = SM_DEC_PASS;  // 8-byte chunks per execution pass (most tags are <= 16 B)
-
 __device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
   if (p + 3 < N && (((uintptr_t)(in + p)) & 3) == 0) return *reinterpret_cast<const uint32_t*>(in + p);
   uint32_t v = 0;
@@ -80,46 +71,45 @@ __device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N,
 // ---------------------------------------------------------------------------------------
 // batched tag engine
 
-// size of a tag starting with byte c followed by `trailer` (u8; 255 = long literal)
-__device__ inline uint32_t spec_size(uint32_t c, uint32_t trailer) {
-  uint32_t entry = char_entry(c);
-  uint32_t taglen = entry >> 11;
-  if (c & 3) return 1 + taglen;
-  uint32_t len = entry & 0xff;
-  uint32_t tr = taglen >= 4 ? trailer : (trailer & ((1u << (8 * taglen)) - 1u));
-  uint32_t lit = len + tr;  // u32 wrap, as the reference
-  return lit > kMaxBatchLit ? 255u : 1 + taglen + lit;
-}
-
-__device__ inline uint32_t pack_sizes_slow(uint32_t cur, uint32_t nxt) {
-  uint32_t s = 0;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    uint32_t c = (cur >> (8 * j)) & 0xff;
-    uint32_t tr = j == 3 ? nxt : __builtin_amdgcn_alignbyte(nxt, cur, j + 1);
-    s |= spec_size(c, tr) << (8 * j);
-  }
-  return s;
-}
-
-// Speculative sizes of tags starting at the 4 bytes of cur (nxt = the 4 bytes after), packed
-// u8, in SWAR: copy-1/2/4 sizes by a v_perm_b32 byte lookup on the kind bits, short literals
-// (len < 61) as hi + 2 per byte.  Only a lane holding a literal tag with length bytes (hi >=
-// 60: rare in text, ~6% of lanes on random bytes) takes the per-byte path.  Equal to
-// pack_sizes_slow for every input (tools/check_tag_sizes.c, run by tests/test_host_logic.py).
+// Speculative size of a tag starting at a window position (u8; 255 = a literal the batch walk
+// leaves to the general path, which decodes any tag): a copy 1 + taglen; a literal without
+// length bytes (hi < 60) 1 + len; one length byte b (tag byte 0xf0) 2 + (b + 1) when that
+// literal is <= kMaxBatchLit bytes, else 255; two to four length bytes (hi >= 61: longer than
+// 256 bytes in a minimal encoding) always 255.  In SWAR: copy sizes by a v_perm_b32 byte
+// lookup on the kind bits, short literals as hi + 2 per byte; a word holding a literal tag byte
+// with length bytes (63% of the text windows: a copy's offset byte 0xf0/f4/f8/fc somewhere in
+// the 256 bytes) fixes those bytes in SWAR too (no per-byte path).  tools/check_tag_sizes.c
+// restates the per-byte definition and checks this form against it (tests/test_host_logic.py).
 __device__ inline uint32_t pack_sizes(uint32_t cur, uint32_t nxt) {
   const uint32_t K = cur & 0x03030303u, H = (cur >> 2) & 0x3f3f3f3fu;
   const uint32_t csz = __builtin_amdgcn_perm(0u, 0x05030200u, K);       // kind 1/2/3 -> 2/3/5
   const uint32_t ml = __builtin_amdgcn_perm(0u, 0x000000ffu, K);        // 0xff per literal byte (kind 0)
-  const uint32_t sz = (csz & ~ml) | ((H + 0x02020202u) & ml);
-  return ((H + 0x44444444u) & 0x80808080u & ml) ? pack_sizes_slow(cur, nxt) : sz;
+  uint32_t sz = (csz & ~ml) | ((H + 0x02020202u) & ml);
+  const uint32_t h60 = (H + 0x44444444u) & 0x80808080u & ml;           // 0x80: a literal with length bytes
+  if (h60) {
+    const uint32_t hm = h60 | (h60 - (h60 >> 7));                       // 0xff there
+    const uint32_t b = __builtin_amdgcn_alignbyte(nxt, cur, 1);         // the byte after each position
+    const uint32_t e = cur ^ 0xf0f0f0f0u;                               // 0 at a one-length-byte tag
+    const uint32_t ne = (((e & 0x7f7f7f7fu) + 0x7f7f7f7fu) | e) & 0x80808080u;  // 0x80: not 0xf0
+    const uint32_t bb = (((b >> 1) & 0x7f7f7f7fu) + 0x1c1c1c1cu) & 0x80808080u;  // 0x80: b >= 200
+    const uint32_t st = ne | bb;                                        // 0x80: size 255
+    const uint32_t sm = st | (st - (st >> 7));
+    const uint32_t v = (b | sm) + (0x03030303u & ~sm);                  // b + 3 (<= 202) or 0xff: no carry
+    sz = (sz & ~hm) | (v & hm);
+  }
+  return sz;
+}
+
+// the literals the batch walk stops at (size 255 above), for a scalar walk's step over them
+__device__ inline bool walk_stop_literal(uint32_t c, uint64_t lit) {
+  return (c & 3) == 0 && ((c >> 2) >= 61 || lit > kMaxBatchLit);
 }
 
 // ring slot write: stream bytes [base, base+256) (word per lane) at ring[(base & 1023)]
 __device__ inline void ring_put(uint8_t* ring, uint32_t base, uint32_t word, uint32_t lane) {
   uint32_t r = base & (kRing - 1);
   reinterpret_cast<uint32_t*>(ring + r)[lane] = word;
-  if (r == 0 && lane < 4) reinterpret_cast<uint32_t*>(ring + kRing)[lane] = word;  // mirror
+  if (r == 0 && lane < kRingMirror / 4) reinterpret_cast<uint32_t*>(ring + kRing)[lane] = word;  // mirror
 }
 
 // 8 stream bytes at pos (aligned dword reads: the mirror covers the 12 bytes past kRing)
@@ -145,82 +135,106 @@ __device__ inline void ring_fill(const uint8_t* __restrict__ in, uint32_t N, uin
 }
 
 // ---- LDS output window --------------------------------------------------------------------
-// The last kWin output bytes of the stream live in a per-wave LDS ring (position x at
-// x mod kWin) besides going to HBM.  Copies whose offset is <= kLdsSrc read their source
-// there, so a batch's dependency rounds cost LDS latency, not an HBM store->load round trip;
-// HBM gets the output in 16-byte blocks when a batch ends (no partial stores).  A batch writes
-// at most kBatchOut bytes, so a source at distance <= kLdsSrc is never overwritten by the
-// batch's own output (kLdsSrc + kBatchOut + margin <= kWin).  Bytes are written with aligned
-// ds_or_b64 pairs into bytes zeroed when the batch starts (a misaligned LDS write/read costs a
-// cycle per lane, tools/lds_bench.hip).
+// The recent output of the stream lives in a per-wave linear LDS window besides going to HBM:
+// output position x at byte x - wbase (wbase a multiple of 16).  Every byte at or past the
+// current output position op is zero when a batch starts, so tags write by or-ing whole 16-byte
+// pieces (five aligned ds_or_b32, the bytes past the tag trimmed to 0) with no read-modify-write
+// races between lanes.  When a batch would write past the window's end, the last kKeep+ bytes
+// move to its start and the rest is zeroed (win_shift: a few 16-byte LDS ops per lane every
+// couple of batches), so a copy source at distance <= op - wbase (>= kKeep right after a shift,
+// growing until the next) is in LDS; older sources are read from HBM, which holds every byte
+// before the window (only the last partial 16-byte block of a batch waits for the next flush,
+// and it is inside the window).  No position ever wraps: reads and writes are plain offsets.
 #ifndef SM_DEC_WIN
-#define SM_DEC_WIN 1024
+#define SM_DEC_WIN 1792
 #endif
-constexpr uint32_t kWin = SM_DEC_WIN;
+constexpr uint32_t kWin = SM_DEC_WIN;  // window bytes (a multiple of 16)
 #ifndef SM_DEC_BOUT
 #define SM_DEC_BOUT 512
 #endif
-constexpr uint32_t kBatchOut = SM_DEC_BOUT;
-constexpr uint32_t kLdsSrc = kWin - kBatchOut - 64;
+constexpr uint32_t kBatchOut = SM_DEC_BOUT;  // most output bytes of one batch
+#ifndef SM_DEC_KEEP
+#define SM_DEC_KEEP 480
+#endif
+constexpr uint32_t kKeep = SM_DEC_KEEP;  // bytes a shift keeps (the least LDS source reach)
+constexpr uint32_t kWinPad = 16;         // bytes before the window (the dword below a piece)
+static_assert(kKeep + 15 + kBatchOut + 32 <= kWin && kKeep >= 80 && kWin % 16 == 0, "window bounds");
 
-// 8 bytes at byte x of an LDS ring of msk+1 bytes (power of 2, 4-aligned base) whose first 8
-// bytes are mirrored past its end: three aligned dword reads and two funnel shifts, no wrap, no
-// branch.  The input ring's mirror is written with its first slot (ring_put); the output window's
-// at the end of every batch (win_mirror): a round reads only bytes final before its batch.
-__device__ inline uint64_t lds_get8m(const uint8_t* bb, uint32_t msk, uint32_t x) {
-  const uint32_t* w = reinterpret_cast<const uint32_t*>(bb + (x & msk & ~3u));
-  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2];
-  return ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, x) << 32) | __builtin_amdgcn_alignbyte(w1, w0, x);
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+// 16 bytes at LDS byte address a + k (k a compile-time multiple of 4): five aligned dword reads,
+// four funnel shifts (v_alignbyte_b32 reads only the low 2 bits of the shift operand)
+__device__ inline uint4 lds_get16(uint32_t a, uint32_t k) {
+  const lds_u32* w = (const lds_u32*)(size_t)((a & ~3u) + k);
+  const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  return make_uint4(__builtin_amdgcn_alignbyte(w1, w0, a), __builtin_amdgcn_alignbyte(w2, w1, a),
+                    __builtin_amdgcn_alignbyte(w3, w2, a), __builtin_amdgcn_alignbyte(w4, w3, a));
 }
 
-__device__ inline uint64_t win_get8(const uint8_t* win, uint32_t x) { return lds_get8m(win, kWin - 1, x); }
+// v with the bytes from len (1..16) on cleared: two 64-bit right shifts of all-ones (amounts in
+// 0..56 for len >= 1) and a select for the high half
+__device__ inline uint4 trim16(uint4 v, uint32_t len) {
+  uint32_t l8 = len << 3;
+  asm("" : "+v"(l8));  // (else 128 - 8 len folds into a quarter-rate multiply)
+  uint64_t mlo, mhi;   // (v_lshrrev_b64 of the inline constant -1: two shifts, not four)
+  asm("v_lshrrev_b64 %0, %1, -1" : "=v"(mlo) : "v"(64 - min(l8, 64u)));
+  asm("v_lshrrev_b64 %0, %1, -1" : "=v"(mhi) : "v"(128 - l8));
+  const bool hi = len > 8;
+  return make_uint4(v.x & (uint32_t)mlo, v.y & (uint32_t)(mlo >> 32), hi ? v.z & (uint32_t)mhi : 0u,
+                    hi ? v.w & (uint32_t)(mhi >> 32) : 0u);
+}
 
-// the window's first 8 bytes to its mirror (after every write of a batch; two lanes)
-__device__ inline void win_mirror(uint8_t* win, uint32_t lane) {
+// or the 16 bytes v (zero past the piece) into the zeroed window at LDS byte address a + k (k a
+// compile-time multiple of 4): the five dwords from (a - 1) & ~3 with t = -a, alignbyte(hi, lo,
+// t) = (hi:lo) >> 8 (t & 3) -- an aligned a shifts the piece one dword up and ors a zero below
+// it (the window's front pad), no selects
+__device__ inline void lds_or16(uint32_t a, uint32_t k, uint4 v) {
+  const uint32_t wa = ((a - 1u) & ~3u) + k, t = 0u - a;
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(v.x, 0u, t);
+  const uint32_t u1 = __builtin_amdgcn_alignbyte(v.y, v.x, t);
+  const uint32_t u2 = __builtin_amdgcn_alignbyte(v.z, v.y, t);
+  const uint32_t u3 = __builtin_amdgcn_alignbyte(v.w, v.z, t);
+  const uint32_t u4 = __builtin_amdgcn_alignbyte(0u, v.w, t);
+  asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4\nds_or_b32 %0, %3 offset:8\nds_or_b32 %0, %4 offset:12\n"
+               "ds_or_b32 %0, %5 offset:16"
+               : : "v"(wa), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4) : "memory");
+}
+
+// the window's first byte at output position wbase = op0 & ~15, all of it zero
+__device__ inline void win_init(uint8_t* win, uint32_t lane) {
+  for (uint32_t u = lane; u < kWin / 16; u += kWave) reinterpret_cast<uint4*>(win)[u] = make_uint4(0, 0, 0, 0);
+}
+
+// move the window so that it starts at nb = (op - kKeep) & ~15: bytes [nb, op) (rounded up to a
+// 16-byte unit -- the bytes past op are zero) to its start, zeros after
+__device__ inline void win_shift(uint8_t* win, uint32_t& wbase, uint32_t op, uint32_t lane) {
+  const uint32_t nb = (op - kKeep) & ~15u;
+  const uint32_t d = nb - wbase, n = (op - nb + 15) >> 4;
+  uint4* w = reinterpret_cast<uint4*>(win);
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (lane < n) v = w[(d >> 4) + lane];  // (every read is issued before the first write)
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  uint32_t* w = reinterpret_cast<uint32_t*>(win);
-  if (lane < 2) w[kWin / 4 + lane] = w[lane];
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-// OR the low cnt (1..8) bytes of v into the (zeroed) window at output position x: two aligned
-// ds_or_b64, branch-free (the second ors 0 when nothing spills: (v >> 1) >> 63 is 0)
-__device__ inline void win_put8(uint8_t* win, uint32_t x, uint64_t v, uint32_t cnt) {
-  v &= ~0ull >> (8 * (8 - cnt));  // (cnt >= 1: a shift of at most 56)
-  uint64_t* w = reinterpret_cast<uint64_t*>(win);
-  const uint32_t sl = x & (kWin - 1), i = sl >> 3, sh = 8 * (sl & 7);
-  __hip_atomic_fetch_or(&w[i], v << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  __hip_atomic_fetch_or(&w[(i + 1) & (kWin / 8 - 1)], (v >> 1) >> (63 - sh), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// zero the window bytes of positions [x, x+len) (to the end of the last 8-byte word), keeping
-// the bytes below x in its word
-__device__ inline void win_zero(uint8_t* win, uint32_t x, uint32_t len, uint32_t lane) {
-  uint64_t* w = reinterpret_cast<uint64_t*>(win);
-  const uint32_t sl = x & (kWin - 1);
-  if ((sl & 7) && lane == 0)
-    __hip_atomic_fetch_and(&w[sl >> 3], (1ull << (8 * (sl & 7))) - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  const uint32_t f = (sl + 7) >> 3, e = (sl + len + 7) >> 3;
-  for (uint32_t k = f + lane; k < e; k += kWave) w[k & (kWin / 8 - 1)] = 0;
+  for (uint32_t u = lane; u < kWin / 16; u += kWave) w[u] = u < n ? v : make_uint4(0, 0, 0, 0);
+  wbase = nb;
 }
 
 // HBM gets the window bytes of output positions [from, to): head bytes up to a 16-byte
 // position boundary, 16-byte blocks, tail bytes
-__device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t from, uint32_t to, uint32_t lane) {
+__device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t wbase, uint32_t from, uint32_t to,
+                                 uint32_t lane) {
   if (to <= from) return;
   const uint32_t h = min((16u - (from & 15u)) & 15u, to - from);
-  if (lane < h) out[from + lane] = win[(from + lane) & (kWin - 1)];
+  if (lane < h) out[from + lane] = win[from + lane - wbase];
   from += h;
   const uint32_t nb = (to - from) >> 4;
   for (uint32_t k = lane; k < nb; k += kWave) {
     const uint32_t x = from + 16 * k;
-    const uint4 v = *reinterpret_cast<const uint4*>(win + (x & (kWin - 1)));
+    const uint4 v = *reinterpret_cast<const uint4*>(win + (x - wbase));
     *reinterpret_cast<du64u*>(out + x) = ((uint64_t)v.y << 32) | v.x;
     *reinterpret_cast<du64u*>(out + x + 8) = ((uint64_t)v.w << 32) | v.z;
   }
   from += nb << 4;
-  if (lane < to - from) out[from + lane] = win[(from + lane) & (kWin - 1)];
+  if (lane < to - from) out[from + lane] = win[from + lane - wbase];
 }
 
 // Tag walk over a 256-byte window by pointer doubling (VALU + LDS, no serial loop).
@@ -228,7 +242,9 @@ __device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t from
 // to the window (window end or N-1, internal.jl:416).  Every lane computes the speculative
 // sizes of its 4 positions (packed u8 in `sizes`, 255 = a literal too long for a batch).
 // J0[p] = p + size(p), clamped to 256 (beyond the window; its row entry maps to itself, so no
-// read is conditional); a long literal or a position at/after rlim is a stop node (J0[p] = p).
+// read is conditional); a long literal is a stop node (J0[p] = p).  Positions at or after rlim
+// need no stops: a chain's positions increase, so the tags before rlim are a prefix of lanes
+// and the final count drops the rest.
 // J_k = J_{k-1} o J_{k-1}, k < 5, in LDS (J5 = J4 o J4 is applied as two J4 reads, which
 // keeps the decoder's LDS at 7.7 KB: 20 waves per CU): 64 tags = chain elements 0..63.
 // Lane t then holds tag t directly -- J_k applied for every set bit k of t -- with its window
@@ -248,7 +264,7 @@ __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt,
   for (int j = 0; j < 4; ++j) {
     const uint32_t p = 4 * lane + j;
     const uint32_t sz = (sizes >> (8 * j)) & 0xff;
-    J[j] = 2 * ((sz == 255 || p >= rlim) ? p : min(p + sz, 256u));  // 256: beyond the window
+    J[j] = 2 * (sz == 255 ? p : min(p + sz, 256u));  // 256: beyond the window
   }
   if (lane < kWalkLevels) jt[lane * kJtRow + 256] = 512;  // every row maps 256 to itself
   *reinterpret_cast<uint2*>(jt + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
@@ -300,12 +316,20 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   ring_fill(in, N, wb, ring, pre1, pre2, lane);
   bool issue_pre2 = false;
   uint32_t op = op0, flushed = op0;  // output produced / already in HBM
+  const uint32_t wlo = op0 & ~15u;   // (the window never starts below the first output block)
+  uint32_t wbase = wlo;              // output position of the window's first byte
+  win_init(win, lane);
+  const uint32_t winA = lds_addr(win), ringA = lds_addr(ring);
+  const bool in_al = (((uintptr_t)in) & 3) == 0;
   const int64_t Nm1 = min((int64_t)N - 1, (int64_t)ip_end);  // parse limit
 
   STAMP_DECL
+  // every batch consumes input (ip strictly increases): more than N batches means the wave is
+  // not whole (a caller that split it) -- a status, never a hang
+  uint32_t guard = N + 1;
   while ((int64_t)ip < Nm1 && op < op_lim) {
     STAMP_COUNT(6, 1)
-    win_mirror(win, lane);  // (the window's first 8 bytes as the previous batch or big literal left them)
+    if (__builtin_expect(--guard == 0, 0)) return kErrDevice;
     if (ip >= wb + 256) {
       if (__builtin_expect(ip < wb + 512, 1)) {
         ring_put(ring, wb + 768, pre1, lane);
@@ -323,6 +347,14 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     // ip+256+200 < wb+768)
     const uint32_t wlim = (int64_t)(ip + 256) < Nm1 ? ip + 256 : (uint32_t)Nm1;
     uint32_t cpos, csz, sizes;
+#if SM_DUP_D & 1
+    {  // (diagnostic) the walk once more, its results dropped: its instruction count
+      uint32_t c2, s2, z2, i2 = ip;
+      asm volatile("" : "+v"(i2));
+      const uint32_t n2 = walk_window(ring_get8(ring, i2 + 4 * lane), wlim - ip, jt, lane, c2, s2, z2);
+      asm volatile("" : : "v"(c2), "v"(s2), "v"(z2), "s"(n2) : "memory");
+    }
+#endif
     const uint32_t ntok = walk_window(ring_get8(ring, ip + 4 * lane), wlim - ip, jt, lane, cpos, csz, sizes);
     uint32_t tpos = 0, ipw = ip, tnext = 0;
     bool big = false;
@@ -339,33 +371,52 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     STAMP(1)
     if (__builtin_expect(ntok != 0, 1)) {
       const bool mine = lane < ntok;
-      const uint64_t hv = ring_get8(ring, mine ? tpos : wb);
-      const uint32_t c = (uint32_t)hv & 0xff;
-      const uint32_t entry = char_entry(c);
-      const uint32_t len = entry & 0xff;
-      const uint32_t taglen = entry >> 11;
-      const uint32_t tr_raw = (uint32_t)(hv >> 8);
-      const uint32_t trailer = taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * taglen)) - 1u));
-      const bool iscopy = (c & 3) != 0;
-      const uint32_t offset = (entry & 0x700) + trailer;
-      const uint32_t litlen = len + trailer;
-      const uint32_t olen = iscopy ? len : litlen;
-      const uint32_t osat = mine ? min(olen, 65537u) : 0u;
-      const uint32_t incl = scan_dpp(osat);
-      const uint32_t opt = op + incl - osat;
-      const uint32_t lsrc = tpos + 1 + taglen;
-      // the reference's checks as selects (no exec branches); same first-failing order
-      int32_t err;
-      {
-        const int64_t avail_out = (int64_t)size - (int64_t)opt;
-        const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
-        const bool e_off = (int64_t)opt <= (int64_t)(uint32_t)(offset - 1u);                              // :499
-        const bool e_cross = opt - offset < frag_lo;
-        const bool e_len = !((len <= 16) & (offset >= 8) & (avail_out >= 16)) & (avail_out < (int64_t)len);  // :505
-        const bool e_lit = (avail_out < (int64_t)litlen) | (avail_in < (int64_t)litlen);                   // :518
+      // one tag per lane: its fields, output offset (wave scan) and the reference's checks as
+      // selects (no exec branches), in the same first-failing order
+      struct TagDec {
+        uint32_t len, taglen, offset, litlen, osat, incl, opt, lsrc;
+        bool iscopy;
+        int32_t err;
+      };
+      auto tag_decode = [&](uint32_t tp) -> TagDec {
+        TagDec d;
+        const uint64_t hv = ring_get8(ring, mine ? tp : wb);
+        const uint32_t c = (uint32_t)hv & 0xff;
+        const uint32_t entry = char_entry(c);
+        d.len = entry & 0xff;
+        d.taglen = entry >> 11;
+        const uint32_t tr_raw = (uint32_t)(hv >> 8);
+        const uint32_t trailer = d.taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * d.taglen)) - 1u));
+        d.iscopy = (c & 3) != 0;
+        d.offset = (entry & 0x700) + trailer;
+        d.litlen = d.len + trailer;
+        const uint32_t olen = d.iscopy ? d.len : d.litlen;
+        d.osat = mine ? min(olen, 65537u) : 0u;
+        d.incl = scan_dpp(d.osat);
+        d.opt = op + d.incl - d.osat;
+        d.lsrc = tp + 1 + d.taglen;
+        const int64_t avail_out = (int64_t)size - (int64_t)d.opt;
+        const int64_t avail_in = (int64_t)N - (int64_t)d.lsrc;
+        const bool e_off = (int64_t)d.opt <= (int64_t)(uint32_t)(d.offset - 1u);                                // :499
+        const bool e_cross = d.opt - d.offset < frag_lo;
+        const bool e_len = !((d.len <= 16) & (d.offset >= 8) & (avail_out >= 16)) & (avail_out < (int64_t)d.len);  // :505
+        const bool e_lit = (avail_out < (int64_t)d.litlen) | (avail_in < (int64_t)d.litlen);                     // :518
         const int32_t ec = e_off ? kErrCopyOffset : (e_cross ? kErrCross : (e_len ? kErrCopyLength : kOk));
-        err = !mine ? kOk : (iscopy ? ec : (e_lit ? kErrLiteral : kOk));
+        d.err = !mine ? kOk : (d.iscopy ? ec : (e_lit ? kErrLiteral : kOk));
+        return d;
+      };
+      const TagDec d = tag_decode(tpos);
+#if SM_DUP_D & 2
+      {  // (diagnostic) the decode once more, its results dropped: its instruction count
+        uint32_t tp = tpos;
+        asm volatile("" : "+v"(tp));
+        const TagDec e = tag_decode(tp);
+        asm volatile("" : : "v"(e.err), "v"(e.incl), "v"(e.lsrc), "v"(e.offset), "v"(e.litlen));
       }
+#endif
+      const uint32_t len = d.len, offset = d.offset, litlen = d.litlen, incl = d.incl, opt = d.opt, lsrc = d.lsrc;
+      const bool iscopy = d.iscopy;
+      const int32_t err = d.err;
       const uint64_t em = ballot(err != kOk);
       if (__builtin_expect(em != 0, 0)) return (int32_t)readlane((uint32_t)err, ctz64(em));
       // cap the batch output at kBatchOut bytes (the window bound; one tag is <= 200 B) and at
@@ -376,121 +427,83 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         ipw = ip + readlane(tnext, nt - 1);
         big = false;  // the next tag is a batch tag inside the window
       }
-      const bool act_t = lane < nt;
       const uint32_t X = readlane(incl, nt - 1);
       STAMP(2)
 
-      win_zero(win, op, X, lane);
+      if (op - wbase + X + 32 > kWin) win_shift(win, wbase, op, lane);  // (uniform)
       const uint32_t O0 = op;
       const uint32_t slo = opt - offset;
       const uint32_t shi = slo + min(len, offset);
-      // a source older than the window's reach comes from HBM -- if HBM already holds all of it
-      // (the last partial 16-byte block before the batch is only in the window)
-      const bool gsrc = !(SM_ABLATE_D & 4) && iscopy && offset > kLdsSrc && shi <= flushed;
+      // a source before the window comes from HBM, which holds it whole: the window starts at
+      // least kKeep bytes before the output (after a shift or a big literal) or at the first
+      // output block, a source ends at most 64 bytes after its start, and every byte before the
+      // batch but the last partial 16-byte block is flushed
+      // (lane sets as SGPR masks: a ballot of a compare is one v_cmp, and inverse_ballot turns a
+      // mask back into a lane predicate for free -- a ballot of a combined bool costs two VALU)
       const uint64_t all = nt == 64 ? ~0ull : ((1ull << nt) - 1);
-      const bool longlit = !iscopy && litlen > 64;
-      uint64_t done = (ballot(longlit) & all) | ~all;
+      const uint64_t copym = ballot(iscopy) & all;
+      const uint64_t longm = ballot(litlen > 64) & ~copym & all;
+      const uint64_t gm = (SM_ABLATE_D & 4) ? 0ull : ballot(slo < wbase) & copym;
+      const bool gsrc = inverse_ballot(gm);
+      uint64_t done = longm | ~all;
       // HBM sources: this wave's earlier flushes (and big literals) must have landed
-      if (!(SM_ABLATE_D & 8) && ballot(act_t && gsrc)) __threadfence_block();
+      if (!(SM_ABLATE_D & 8) && gm) __threadfence_block();
 
       // long literals (65..200 B, no dependencies, inside the input ring): whole-wave passes
-      uint64_t lm = ballot(act_t && longlit);
+      uint64_t lm = longm;
       while (lm) {
         const uint32_t t = ctz64(lm);
         lm &= lm - 1;
         const uint32_t o = readlane(opt, t), sr = readlane(lsrc, t), L = readlane(litlen, t);
-        const uint32_t k = 8 * lane;
-        if (k < L) win_put8(win, o + k, ring_get8(ring, sr + k), min(8u, L - k));
+        const uint32_t k = 16 * lane;
+        if (k < L) lds_or16(winA + (o - wbase) + k, 0, trim16(lds_get16(ringA + ((sr + k) & (kRing - 1)), 0), min(16u, L - k)));
       }
 
       STAMP(3)
-      // One round (all in LDS) runs every tag whose source is final before the batch; its
-      // writes never touch bytes another ready tag reads:
-      //  * literal (<= 64 B): 8-byte pieces of the input ring;
-      //  * copy: its source window S = out[slo, slo+offset) is final when the round starts, and
-      //    output byte j is S[j mod offset] (incremental_copy_slow!, internal.jl:477-481), so
-      //    chunk i = S from phase m = 8i mod offset, wrapping once to S's start (offset >= 8);
-      //    for offset < 8 the period is unrolled to 16 bytes in registers.
+      // One round (all in LDS, or HBM for sources before the window) runs every tag whose source
+      // is final before the batch and whose bytes can be read straight: a literal (<= 64 B, from
+      // the input ring) or a copy with offset >= 16 -- output byte j is S[j mod offset]
+      // (incremental_copy_slow!, internal.jl:477-481), which for j >= offset is the copy's own
+      // output byte j - offset = out[slo + j], written by an earlier 16-byte pass.  So every tag
+      // reads out[slo + j] (or its literal bytes) in 16-byte pieces.  The writes never touch
+      // bytes another ready tag reads.
       if (SM_ABLATE_D & 1) done = ~0ull;
       if (__builtin_expect(done != ~0ull, 1)) {
         STAMP_COUNT(7, 1)
-        const bool ready = !((done >> lane) & 1) && ((SM_ABLATE_D & 2) || !iscopy || shi <= O0);
-        const uint64_t rm = ballot(ready);
+        const uint64_t rm = ~done & ((SM_ABLATE_D & 2) ? ~0ull : ~copym | (ballot(shi <= O0) & ballot(offset >= 16)));
         const uint32_t L = iscopy ? len : litlen;
-        // HBM sources near the stream's end (a copy to its last 8 bytes) are read through
-        // out_get8, which stops at the copy's destination; every other batch keeps plain loads
-        const bool gtail = ballot(ready && gsrc && opt + 8 > size) != 0;
-        auto rounds = [&](auto tailc) {
-          auto gload = [&](uint32_t p) -> uint64_t {
-            if constexpr (decltype(tailc)::value) return out_get8(out, p, opt);
-            else return *reinterpret_cast<const du64u*>(out + p);
-          };
-          for (uint32_t base = 0; base < 64; base += 8 * kPass) {
-            const bool act = ready && L > base;
-            if (!ballot(act)) break;
-            if (act) {
-              uint64_t v[kPass];
-              if (!iscopy || offset >= 8) {
-                // a literal (input ring; it never wraps) or a copy with offset >= 8 (output window,
-                // or HBM for far sources): 8-byte pieces of S, wrapping once to S's start
-                const uint8_t* bb = iscopy ? win : ring;
-                const uint32_t msk = iscopy ? kWin - 1 : kRing - 1;
-                const uint32_t sp = iscopy ? slo : lsrc;
-                const uint32_t off = iscopy ? offset : 0xffffu;
-                // S's first 8 bytes, needed only when S wraps inside this pass (offset < base + 16)
-                uint64_t B = 0;
-                if (off < base + 8 * kPass) B = gsrc ? gload(slo) : lds_get8m(bb, msk, sp);
-                uint32_t m0 = base;
-                while (m0 >= off) m0 -= off;
-                uint32_t m = m0;
+        const uint32_t sa = iscopy ? winA + (slo - wbase) : ringA + (lsrc & (kRing - 1));
+        const uint32_t da = winA + (opt - wbase);
+        const uint8_t* gs = out + slo;
+#if SM_DUP_D & 8
+        for (int dup = 0; dup < 2; ++dup) {  // (diagnostic) the round twice: or-ing the same bytes again changes nothing
+          asm volatile("" : : : "memory");
+#endif
 #pragma unroll
-                for (int i = 0; i < kPass; ++i) {
-                  v[i] = base + 8 * i < L ? (gsrc ? gload(slo + m) : lds_get8m(bb, msk, sp + m))
-                                          : 0ull;
-                  m += 8;
-                  if (m >= off) m -= off;
-                }
-                m = m0;
-#pragma unroll
-                for (int i = 0; i < kPass; ++i) {
-                  const uint32_t keep = off - m;  // bytes of this chunk before S wraps
-                  if (keep < 8) v[i] = (v[i] & ((1ull << (8 * keep)) - 1)) | (B << (8 * keep));
-                  m += 8;
-                  if (m >= off) m -= off;
-                }
-              } else {
-                const uint64_t x = win_get8(win, slo);
-                uint64_t p0 = x & ((1ull << (8 * offset)) - 1);
-                for (uint32_t have = offset; have < 8; have *= 2) p0 |= p0 << (8 * have);
-                // p0 = S repeated over 8 bytes; p1 = the next 8 bytes of the period
-                uint32_t e = 8;
-                while (e >= offset) e -= offset;
-                // p1[k] = seq[8+k] = p0[e+k] (e+k < 8) or p0[e+k-offset] (e+k >= 8)
-                const uint64_t hib = e ? ~0ull << (8 * (8 - e)) : 0ull;
-                const uint64_t p1 = e ? ((p0 >> (8 * e)) | ((p0 << (8 * (offset - e))) & hib)) : p0;
-                uint32_t m = base;
-                while (m >= offset) m -= offset;
-#pragma unroll
-                for (int i = 0; i < kPass; ++i) {
-                  v[i] = m ? ((p0 >> (8 * m)) | (p1 << (8 * (8 - m)))) : p0;
-                  m += 8;
-                  while (m >= offset) m -= offset;
-                }
-              }
-#pragma unroll
-              for (int i = 0; i < kPass; ++i)
-                if (base + 8 * i < L) win_put8(win, opt + base + 8 * i, v[i], min(8u, L - base - 8 * i));
+        for (uint32_t base = 0; base < 64; base += 16) {
+          const uint64_t am = rm & ballot(L > base);
+          if (!am) break;
+          if (inverse_ballot(am)) {
+            uint4 v;
+            if (gsrc) {
+              const du64u* g = reinterpret_cast<const du64u*>(gs + base);
+              const uint64_t a = g[0], b = g[1];
+              v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+            } else {
+              v = lds_get16(sa, base);
             }
+            lds_or16(da, base, trim16(v, min(L - base, 16u)));
           }
-        };
-        if (__builtin_expect(gtail, 0)) rounds(std::true_type{});
-        else rounds(std::false_type{});
+        }
+#if SM_DUP_D & 8
+        }
+#endif
         done |= rm;
       }
       STAMP(8)
       STAMP_COUNT(9, __builtin_popcountll(~done))
-      // The copies left (a few per batch: their source overlaps earlier tags of this batch) run
-      // in stream order, one tag at a time, a byte per lane: byte k = S[k mod offset] with S
+      // The copies left -- their source overlaps earlier tags of this batch, or offset < 16 --
+      // run in stream order, one tag at a time, a byte per lane: byte k = S[k mod offset] with S
       // final by then (LDS accesses of a wave are serviced in order).
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       uint64_t rest = ~done;
@@ -505,19 +518,25 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
             const uint32_t q = (uint32_t)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)off));
             k -= q * off;
           }
-          win[(o + lane) & (kWin - 1)] = win[(sl + k) & (kWin - 1)];
+          win[o + lane - wbase] = win[sl + k - wbase];
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
       }
       STAMP(4)
       op += X;
       if (__builtin_expect(op > op_lim, 0)) return kErrCross;  // a tag crosses the fragment end
-      win_flush(out, win, flushed, op & ~15u, lane);  // whole 16-byte blocks to HBM
+      win_flush(out, win, wbase, flushed, op & ~15u, lane);  // whole 16-byte blocks to HBM
+#if SM_DUP_D & 4
+      asm volatile("" : : : "memory");
+      win_flush(out, win, wbase, flushed, op & ~15u, lane);  // (diagnostic) the same bytes again
+#endif
       flushed = max(flushed, op & ~15u);
       ip = ipw;
     }
     if (issue_pre2) {
-      pre2 = load_word(in, N, wb + 1024 + 4 * lane);
+      // (a whole slot inside the stream at a 4-aligned base: one plain load, the test uniform)
+      pre2 = (in_al && wb + 1280 <= N) ? reinterpret_cast<const uint32_t*>(in + wb + 1024)[lane]
+                                       : load_word(in, N, wb + 1024 + 4 * lane);
       issue_pre2 = false;
     }
 
@@ -535,7 +554,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
       if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) return kErrLiteral;  // :518
       if ((uint64_t)op + litlen > op_lim) return kErrCross;
-      win_flush(out, win, flushed, op, lane);  // HBM holds everything before the literal
+      win_flush(out, win, wbase, flushed, op, lane);  // HBM holds everything before the literal
       // bulk copy: head bytes to 16-B source alignment, then 16 B per lane, 4 in flight
       const uint8_t* s = in + lsrc;
       uint32_t head = (uint32_t)((16 - ((uintptr_t)s & 15)) & 15);
@@ -563,29 +582,40 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       }
       const uint32_t done16 = head + (n16 << 4);
       if (lane < litlen - done16) out[op + done16 + lane] = s[done16 + lane];
-      // the window keeps the literal's tail, which later copies may read: every slot, since a
-      // copy that depends on the next batch's own output reads the window at offsets up to
-      // kBatchOut + 64 (more than kLdsSrc with a small window)
-      const uint32_t keep = min(litlen, kWin);
-      const uint32_t t0 = op + litlen - keep;
-      win_zero(win, t0, keep, lane);
-      for (uint32_t x = 8 * lane; x < keep; x += 8 * kWave) {
-        const uint8_t* q = s + (t0 - op) + x;
-        const uint32_t cnt = min(8u, keep - x);
-        uint64_t v = 0;
-        if (cnt == 8) {
-          v = *reinterpret_cast<const du64u*>(q);
-        } else {  // the literal's last bytes: never read past the stream
-          for (uint32_t i = 0; i < cnt; ++i) v |= (uint64_t)q[i] << (8 * i);
+      // the window restarts at nb = the 16-byte output boundary at or below op + litlen - kKeep
+      // (not below the decode's first output block), filled from HBM -- which now holds all
+      // output before op + litlen -- with zeros past op + litlen (any literal length, a wrapped
+      // 0 included); older sources come from HBM
+      const uint32_t opn = op + litlen;
+      const uint32_t nb = (opn - min(opn - wlo, kKeep)) & ~15u;
+      const uint32_t nk = opn - nb;
+      __threadfence_block();  // (this wave's stores above land before the loads below)
+      const uint8_t* q = out + nb;
+      for (uint32_t u = lane; u < kWin / 16; u += kWave) {
+        const uint32_t x = 16 * u;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (x + 16 <= nk) {
+          const du64u* g = reinterpret_cast<const du64u*>(q + x);
+          const uint64_t a = g[0], b = g[1];
+          v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+        } else if (x < nk) {  // the last bytes: never read past the output
+          uint64_t lo = 0, hi = 0;
+          for (uint32_t i = 0; i < nk - x; ++i) {
+            const uint64_t bt = (uint64_t)q[x + i] << (8 * (i & 7));
+            if (i < 8) lo |= bt;
+            else hi |= bt;
+          }
+          v = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
         }
-        win_put8(win, t0 + x, v, cnt);
+        reinterpret_cast<uint4*>(win)[u] = v;
       }
+      wbase = nb;
       op += litlen;
       flushed = op;
       ip = lsrc + litlen;
     }
   }
-  win_flush(out, win, flushed, op, lane);
+  win_flush(out, win, wbase, flushed, op, lane);
   STAMP(5)
   STAMP_FLUSH(g_stamp)
   op_end = op;
@@ -621,14 +651,11 @@ __device__ inline int32_t parse_header(const uint8_t* in, uint32_t N, uint32_t l
 }
 
 #ifndef SM_DEC_OCC
-#define SM_DEC_OCC 7  // waves per SIMD: 68 VGPRs, 4.7 KB LDS per wave
+#define SM_DEC_OCC 7  // waves per SIMD: 69 VGPRs, 5.6 KB LDS per wave
 #endif
-__global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
-  __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];  // tag-walk jump tables
-  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin + 16];           // output window (+ mirror)
-  const uint32_t lane = lane_id();
-  const uint32_t b = blockIdx.x;
+// one stream of the batch (block b) by one wave
+__device__ inline void decompress_block(const DecompressArgs& a, uint32_t b, uint8_t* sring, uint16_t* sjt, uint8_t* swin,
+                                        uint32_t lane) {
   const uint8_t* in = a.one_n ? a.in : a.in + a.in_off[b];
   const uint32_t N = a.one_n ? a.one_n : a.in_len[b];
   uint8_t* dst = a.one_n ? a.out : a.out + a.out_off[b];
@@ -654,6 +681,40 @@ __global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a)
     a.out_len[b] = st == kOk ? size : 0;
   }
 }
+
+__global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + kRingMirror];
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];  // tag-walk jump tables
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWinPad + kWin];  // output window
+  decompress_block(a, blockIdx.x, sring, sjt, swin + kWinPad, lane_id());
+}
+
+#if SM_DEC_QUEUE
+// Diagnostic variant: persistent waves taking streams from a global
+// counter.  The grab is lane 0's atomic add made wave-uniform by v_readfirstlane -- the round-4
+// variant's hang came from a grab that was not: decode_stream_batch needs the whole wave (its
+// walk reads other lanes through ds_bpermute, and an inactive lane reads 0), so a wave split by
+// a per-lane grab computes no tags, makes no progress and loops.  Bounded twice: at most nblk + 1
+// grabs per wave, and decode_stream_batch gives up with kErrDevice after N batches.  The host
+// zeroes the counter before each launch (sm_api.hip).
+__device__ unsigned int g_dec_queue;
+__global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress_q(DecompressArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + kRingMirror];
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWinPad + kWin];
+  const uint32_t lane = lane_id();
+  for (uint32_t it = 0; it <= a.nblk; ++it) {
+    uint32_t b = 0;
+    if (lane == 0) b = atomicAdd(&g_dec_queue, 1u);
+    b = uniform(b);
+#if SM_DEC_QUEUE > 1
+    if (__builtin_amdgcn_readlane(b, 63) != b) printf("k_decompress_q: wave grab not uniform (%u)\n", b);
+#endif
+    if (b >= a.nblk) break;
+    decompress_block(a, b, sring, sjt, swin + kWinPad, lane);
+  }
+}
+#endif
 
 // ---- one large stream, decoded in parallel ------------------------
 // Snappy.jl (src/Snappy.jl:29-33), libsnappy and this library compress 64 KiB blocks
@@ -862,7 +923,7 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
           done = true;
         } else {
           tag_at(buf, (uint32_t)x, size, outb);
-          if ((buf[x] & 3) == 0 && outb > kMaxBatchLit) {
+          if (walk_stop_literal(buf[x], outb)) {
             pre += (uint32_t)outb;
             x += size;
             again = true;
@@ -938,9 +999,9 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
 
 __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
                                                             uint8_t* out, const StreamFrag* frags, int32_t* status) {
-  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + kRingMirror];
   __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];
-  __shared__ __attribute__((aligned(16))) uint8_t swin[kWin + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWinPad + kWin];
   __shared__ __attribute__((aligned(16))) uint8_t sbuf[kIdxChunk + kIdxPad];
   const uint32_t f = blockIdx.x, lane = lane_id();
   const StreamFrag fr = frags[f];
@@ -977,7 +1038,7 @@ __global__ __launch_bounds__(64, 4) void k_decompress_frags(const uint8_t* __res
   if (st == kOk && o != fr.F) st = kErrCross;  // no tag starts at F: not block-structured
   if (st == kOk) {
     uint32_t op_end = 0;
-    st = decode_stream_batch(in, N, (uint32_t)p, N, size, out, fr.F, fr.F, sring, sjt, swin, lane, op_end, fr.lim);
+    st = decode_stream_batch(in, N, (uint32_t)p, N, size, out, fr.F, fr.F, sring, sjt, swin + kWinPad, lane, op_end, fr.lim);
     if (st == kOk && op_end != (fr.lim == 0xffffffffu ? size : fr.lim)) st = kErrCross;
   }
   if (lane == 0) status[f] = st;
@@ -1485,6 +1546,15 @@ hipError_t launch_decompress_frags(const uint8_t* in, uint32_t N, uint32_t size,
 
 hipError_t launch_decompress(const DecompressArgs& a, int /*large*/, hipStream_t s) {
   if (a.nblk == 0) return hipSuccess;
+#if SM_DEC_QUEUE
+  if (!a.one_n) {  // (diagnostic build) one wave per resident slot: 256 CUs x 4 SIMDs x SM_DEC_OCC
+    const unsigned int zero = 0;
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dec_queue), &zero, sizeof(zero), 0, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_decompress_q, dim3(min(a.nblk, 256u * 4u * SM_DEC_OCC)), dim3(64), 0, s, a);
+    return hipGetLastError();
+  }
+#endif
   hipLaunchKernelGGL(k_decompress, dim3(a.nblk), dim3(64), 0, s, a);
   return hipGetLastError();
 }

@@ -129,6 +129,9 @@ __device__ inline uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __b
 
 __device__ inline uint64_t ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
+// the lane predicate of an SGPR lane mask (free: the mask is the predicate)
+__device__ inline bool inverse_ballot(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
 __device__ inline uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 __device__ inline uint32_t readlane(uint32_t v, uint32_t l) { return __builtin_amdgcn_readlane(v, l); }
@@ -160,6 +163,11 @@ __device__ inline uint32_t scan_dpp(uint32_t v) {
 // v_alignbyte_b32.  A misaligned ds_read_b32/b64 is serviced one lane per LDS cycle (~64
 // cycles per wave-instruction) against 2-8 aligned and ~15 for this form on random
 // addresses (tools/lds_bench.hip, measured on MI355X).
+// the LDS byte address of a pointer into a __shared__ array
+__device__ inline uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 // lds_ld32: the array must have >= 4 readable bytes past pos+3.
 __device__ inline uint32_t lds_ld32(const uint8_t* lds, uint32_t pos) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (pos & ~3u));

@@ -443,6 +443,55 @@ def test_decompress_random_op_streams(sm, gpu_available):
         assert o == expect
 
 
+def _nonminimal_streams(seed, count):
+    """Streams whose literal tags carry 1..4 length bytes whatever the length (hi = 59 + k), a
+    wrapped 4-byte length (1 + 0xffffffff = 0 in UInt32, internal.jl:456), and copies reaching
+    back across them (LDS window and HBM sources)."""
+    from streams import copy_tag, lit_tag, varint
+    rng = np.random.default_rng(seed)
+    streams = []
+    for _ in range(count):
+        body, out = bytearray(), bytearray()
+        target = int(rng.integers(1, 20000))
+        while len(out) < target:
+            r = rng.random()
+            if not out or r < 0.35:
+                n = int(rng.choice([1, 2, 15, 16, 17, 60, 61, 64, 65, 100, 199, 200, 201, 300, 700]))
+                data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+                k = int(rng.integers(1, 5))
+                if n - 1 >= 1 << (8 * k):
+                    body += lit_tag(n)
+                else:
+                    body += bytes([(59 + k) << 2]) + (n - 1).to_bytes(k, "little")
+                body += data
+                out += data
+            elif r < 0.38:
+                body += bytes([63 << 2]) + b"\xff\xff\xff\xff"  # a wrapped length: 0 bytes
+            else:
+                off = int(rng.integers(1, min(len(out), 3000) + 1))
+                ln = int(rng.integers(1, 65))
+                body += copy_tag(off, ln)
+                for _ in range(ln):
+                    out.append(out[-off])
+        streams.append((varint(len(out)) + bytes(body), bytes(out)))
+    return streams
+
+
+def test_decompress_nonminimal_literals(sm, oracle, gpu_available):
+    """Literal tags with more length bytes than needed (the batch walk leaves every hi >= 61
+    literal to the general path and sizes hi = 60 ones in SWAR: sm_decompress.hip pack_sizes,
+    tools/check_tag_sizes.c) and wrapped lengths, between copies: outputs equal the LZ77
+    meaning and the oracle's, in one batch and through validate."""
+    built = _nonminimal_streams(77, 300)
+    outs = _decode_all(sm, [s for s, _ in built])
+    for (s, expect), o in zip(built, outs):
+        assert o == expect
+        assert oracle.uncompress(s) == expect
+    for s, expect in built[:40]:
+        assert sm.validate(s) == 0
+        assert sm.uncompress(s) == expect
+
+
 # ---- one large stream: parallel fragment decode (sm_uncompress) ---------------------------
 
 def _big_corpus(n):
