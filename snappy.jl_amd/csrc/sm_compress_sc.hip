@@ -248,8 +248,10 @@ __device__ inline uint4 sc_trim(uint4 v, uint32_t len) {
 __device__ inline uint4 sc_trim1(uint4 v, uint32_t len) {
   uint32_t l8 = len << 3;
   asm("" : "+v"(l8));  // (else the compiler folds 128 - 8 len into a quarter-rate multiply by 56)
-  const uint64_t mlo = ~0ull >> (64 - min(l8, 64u));
-  const uint64_t mhi = ~0ull >> (128 - l8);  // (v_lshrrev_b64 reads 6 bits; len > 8: 0..56)
+  uint64_t mlo, mhi;  // (v_lshrrev_b64 of the inline constant -1 reads 6 bits of the amount; len > 8: 0..56;
+                      // written out, the compiler splits the halves into four shifts)
+  asm("v_lshrrev_b64 %0, %1, -1" : "=v"(mlo) : "v"(64 - min(l8, 64u)));
+  asm("v_lshrrev_b64 %0, %1, -1" : "=v"(mhi) : "v"(128 - l8));
   const bool hi = len > 8;
   return make_uint4(v.x & (uint32_t)mlo, v.y & (uint32_t)(mlo >> 32), hi ? v.z & (uint32_t)mhi : 0u,
                     hi ? v.w & (uint32_t)(mhi >> 32) : 0u);

@@ -382,11 +382,15 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         TagDec d;
         const uint64_t hv = ring_get8(ring, mine ? tp : wb);
         const uint32_t c = (uint32_t)hv & 0xff;
-        const uint32_t entry = char_entry(c);
+        const uint32_t entry = char_entry(c);  // (a 512-byte table in global memory instead: 1.510 against 1.455 ms)
         d.len = entry & 0xff;
         d.taglen = entry >> 11;
         const uint32_t tr_raw = (uint32_t)(hv >> 8);
-        const uint32_t trailer = d.taglen >= 4 ? tr_raw : (tr_raw & ((1u << (8 * d.taglen)) - 1u));
+        // the low taglen bytes (0..4) of tr_raw: the low dword of ~0 << 8 taglen (64-bit: 0 for 4)
+        // clears them in a mask, one v_bfi_b32 keeps them
+        uint64_t hm;
+        asm("v_lshlrev_b64 %0, %1, -1" : "=v"(hm) : "v"(8 * d.taglen));
+        const uint32_t trailer = tr_raw & ~(uint32_t)hm;
         d.iscopy = (c & 3) != 0;
         d.offset = (entry & 0x700) + trailer;
         d.litlen = d.len + trailer;

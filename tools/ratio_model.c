@@ -19,6 +19,8 @@
 //   SCS=n      super-chunk bytes (1024)
 //   HASH=1     the full-rate hash of round 5: ((w ^ (w >> 15)) * 0x9e3779 as u24 x u24) >> (32 - b)
 //   POS0=1     slots hold positions (not position + 1): an empty slot is candidate 0 (verified)
+//   SPARSE=1   only even positions are hashed and inserted; an odd position q - 1 takes the even
+//              q's candidate c as c - 1 when the byte before it matches (a 5-byte match)
 // Prints per file: the model's size, the size the reference's parse gives (the oracle), the ratio.
 // Build: gcc -O2 -o /tmp/rm tools/ratio_model.c -L oracle -loracle_snappy -Wl,-rpath,$PWD/oracle
 // Run:   [FAR=256] /tmp/rm tests/golden/testdata/{alice29.txt,...}
@@ -32,7 +34,7 @@ static uint32_t ld32(const uint8_t* p) {
   memcpy(&v, p, 4);
   return v;
 }
-static int hashmode = 0, pos0 = 0;
+static int hashmode = 0, pos0 = 0, sparse = 0;
 static int farmax = 1 << 30, blk = 65536, longnear = 0, margin = 0, tbits = 13, far_d = 256, longest = 0, long8 = 0, long16 = 0, xsc = 0, merge = 0, scs = 1024;
 
 static uint32_t lit_bytes(uint32_t n) { return n == 0 ? 0 : n + (n <= 60 ? 1 : (n <= 256 ? 2 : (n <= 65536 ? 3 : 4))); }
@@ -56,9 +58,10 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
   static uint32_t cand[65536];
   static uint8_t has[65536];
   memset(T, 0, sizeof T);
+  for (uint32_t q = 0; q < n; ++q) has[q] = 0;
   for (uint32_t q = 0; q < n; ++q) {
-    has[q] = 0;
     if (q + 4 > n) continue;
+    if (sparse && (q & 1)) continue;
     const uint32_t w = ld32(b + q);
     uint32_t h;
     if (hashmode == 1) h = (((w ^ (w >> 15)) & 0xffffffu) * 0x9e3779u) >> (32 - tbits);
@@ -93,6 +96,10 @@ static uint64_t block_bytes(const uint8_t* b, uint32_t n) {
     }
     has[q] = 1;
     cand[q] = use2 ? p2 : p1;
+    if (sparse && q > 0 && cand[q] > 0 && b[cand[q] - 1] == b[q - 1]) {
+      has[q - 1] = 1;
+      cand[q - 1] = cand[q] - 1;
+    }
     g_both[q] = m1 && m2;
     {
       const uint32_t lim16 = q + 16 < n ? q + 16 : n;
@@ -157,6 +164,7 @@ int main(int argc, char** argv) {
   if (getenv("SCS")) scs = atoi(getenv("SCS"));
   if (getenv("HASH")) hashmode = atoi(getenv("HASH"));
   if (getenv("POS0")) pos0 = atoi(getenv("POS0"));
+  if (getenv("SPARSE")) sparse = atoi(getenv("SPARSE"));
   double worst = 0, tot_m = 0, tot_r = 0;
   for (int f = 1; f < argc; ++f) {
     FILE* fp = fopen(argv[f], "rb");
