@@ -236,7 +236,7 @@ class StreamShard:
         # the global index: a real stream length (not poisoned by an error mark, dist.py), and
         # offsets strictly increasing by this rank's sizes
         ok = ok and self.stream_len is not None and int(self.stream_len.item()) > 0
-        if self.nfrag > 1:
+        if self.nfrag > 1 and self.offsets is not None:
             d = self.offsets[1:] - self.offsets[:-1]
             ok = ok and bool(torch.equal(d, self.comp_len[:-1].to(torch.int64)))
         return ok

@@ -69,6 +69,7 @@ def fragments(sm, dev, args):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.reps
     print("%s: %.3f ms/launch, %.2f GB/s (uncompressed bytes)" % (args.op, dt * 1e3, sh.in_bytes / dt / 1e9))
+    sh.index(bench.load_dist(), 0, 1)  # (world 1, no process group: the scan alone)
     print("roundtrip ok:", sh.verify(sm))
 
 

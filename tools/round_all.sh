@@ -9,4 +9,4 @@ tail -3 $O/pytest_gpu.log
 [ $rc = 0 ] || { echo "pytest rc $rc"; exit 1; }
 timeout -k 10 400 python bench.py --extras > $O/bench.json 2> $O/bench.err || { echo bench failed; tail $O/bench.err; exit 1; }
 cat $O/bench.json
-bash tools/profile_round.sh $R || exit 1
+[ "${SKIP_PROF:-0}" = 1 ] || bash tools/profile_round.sh $R || exit 1
