@@ -48,6 +48,12 @@ struct DevBuf {
 // into the device (dp): the single-buffer calls' last kernel writes its result there directly,
 // because a copy-engine transfer queued behind kernels waited up to ~120 us on this box
 // (tools/probes/latency_probe.hip, profiles/r04_latency_probe.txt).
+// Visibility: kernels store results into this memory and the host reads them only after
+// hipStreamSynchronize on the launching stream; HIP makes a kernel's writes to host memory visible
+// to the host at that synchronisation (the completion signal is a system-scope release), so the
+// writers issue no fence of their own.  A __threadfence_system() in each writer
+// was measured in round 5: every wave writes back the L2 (buffer_wbl2), and single calls took
+// 20-45 us longer (alice29.txt compress 60 -> 104 us, urls.10K uncompress 296 -> 527 us, same box).
 struct HostBuf {
   void* p = nullptr;
   void* dp = nullptr;  // the device's address of p (nullptr: not mapped)

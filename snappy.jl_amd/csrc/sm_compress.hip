@@ -468,7 +468,6 @@ __global__ __launch_bounds__(256) void k_gather16(const uint8_t* __restrict__ sr
   __syncthreads();
   if (sh[1]) return;
   gather_unit(src + src_off[b], len[b], dst + sh[0], blockIdx.y, gridDim.y);
-  __threadfence_system();  // (dst: device-mapped host memory, read after the synchronisation)
 }
 
 // k_gather16 for the parts of k_compress_sc_span: unit u = part u % parts of block u / parts (one
@@ -525,7 +524,6 @@ __global__ __launch_bounds__(256) void k_gather_parts(const uint8_t* __restrict_
     }
     gather_unit(in + in_off[b], n, g + tb, blockIdx.y, gridDim.y);
   }
-  __threadfence_system();  // (dst: device-mapped host memory, read after the synchronisation)
 }
 
 hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,

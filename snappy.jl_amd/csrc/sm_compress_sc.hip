@@ -847,22 +847,13 @@ __device__ __attribute__((always_inline)) inline void sc_copy_out(uint8_t* const
   const uint32_t ad = (uint32_t)((uintptr_t)g & 15);
   const uint32_t u0 = ad ? 1u : 0u, u1 = (len + ad) >> 4;  // full units [u0, u1); unit u = bytes [16u - ad, +16)
   uint4* const g16 = reinterpret_cast<uint4*>(g - ad);
-  const uint4* const s16 = reinterpret_cast<const uint4*>(stg);
-  const uint32_t sb = (16 - ad) & 15, dw = sb >> 2, bs = sb & 3;  // a unit starts sb bytes into a staging unit
+  const uint32_t* const s32 = reinterpret_cast<const uint32_t*>(stg);
   for (uint32_t u = u0 + lane; u < u1; u += 64) {
-    const uint32_t j = 16 * u - ad;  // staging offset of the unit
-    const uint4 A = s16[j >> 4], B = s16[(j >> 4) + 1];
-    const uint32_t x[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-    uint32_t r5[5];
-#pragma unroll
-    for (int t = 0; t < 5; ++t) {
-      uint32_t vv = x[t];
-#pragma unroll
-      for (int dd = 1; dd < 4; ++dd) vv = dw == (uint32_t)dd ? x[t + dd] : vv;
-      r5[t] = vv;
-    }
-    g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r5[1], r5[0], bs), __builtin_amdgcn_alignbyte(r5[2], r5[1], bs),
-                        __builtin_amdgcn_alignbyte(r5[3], r5[2], bs), __builtin_amdgcn_alignbyte(r5[4], r5[3], bs));
+    const uint32_t j = 16 * u - ad;  // staging offset of the unit: five aligned dwords from j & ~3, funnel shifts
+    const uint32_t* w = s32 + (j >> 2);  // (j + 20 <= len + 4: inside the slot)
+    const uint32_t r0 = w[0], r1 = w[1], r2 = w[2], r3 = w[3], r4 = w[4];
+    g16[u] = make_uint4(__builtin_amdgcn_alignbyte(r1, r0, j), __builtin_amdgcn_alignbyte(r2, r1, j),
+                        __builtin_amdgcn_alignbyte(r3, r2, j), __builtin_amdgcn_alignbyte(r4, r3, j));
   }
   const uint32_t nh = min(u0 ? 16 - ad : 0u, len);              // head bytes [0, nh)
   const uint32_t tb = max(16 * u1 > ad ? 16 * u1 - ad : 0u, nh);  // tail bytes [tb, len)

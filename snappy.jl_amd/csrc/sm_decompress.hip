@@ -1418,7 +1418,6 @@ __global__ __launch_bounds__(256) void k_small_resolve(const uint8_t* __restrict
   if (r == 0 && t0 == 0) {
     words[0] = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     words[1] = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __threadfence_system();
   }
   if (small_failed(ctl)) return;
   if (r > 0 && __hip_atomic_load(&pend[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
@@ -1443,7 +1442,6 @@ __global__ __launch_bounds__(256) void k_small_resolve(const uint8_t* __restrict
   // third verdict word (the host zeroes it before the call; every writer writes 1), so the host falls
   // back instead of returning bytes this call never wrote
   if (last && any_left && lane_id() == 0) words[2] = 1u;
-  __threadfence_system();  // (out and words may be device-mapped host memory)
 }
 
 __global__ __launch_bounds__(256) void k_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending) {
@@ -1475,7 +1473,6 @@ __global__ __launch_bounds__(256) void k_to_host(const uint8_t* __restrict__ src
   for (uint32_t i = t; i < n16; i += gridDim.x * blockDim.x)
     reinterpret_cast<uint4*>(dst)[i] = reinterpret_cast<const uint4*>(src)[i];
   if (t < n - 16 * n16) dst[16 * n16 + t] = src[16 * n16 + t];
-  __threadfence_system();  // (dst and words are device-mapped host memory, read after the synchronisation)
 }
 
 hipError_t launch_to_host(const uint8_t* src, uint32_t n, uint8_t* dst, const uint32_t* wsrc, uint32_t nw,
