@@ -99,6 +99,9 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #ifndef SC_GC
 #define SC_GC 0
 #endif
+#ifndef SC_WPRE  // the writer reads the next slot's size word with this slot's bytes
+#define SC_WPRE 1
+#endif
 #ifndef SC_CB  // fast mode: section C's groups per batch of candidate loads in flight
 #define SC_CB 2
 #endif
@@ -875,11 +878,19 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, uint32
                                                                uint32_t* len_out, uint32_t lane) {
   uint32_t o = hv, err = 0;
   STAMP_DECL
+  // (the next slot's size word is read together with this slot's bytes: when the workers are ahead,
+  // as they mostly are, the next link starts without a poll round trip of its own)
+  uint32_t vpre = 0;
   for (uint32_t k = k0; k < k1; ++k) {
     const uint32_t slot = k % kScRing;
-    const uint32_t sz = sc_wait(&S.rsize[slot], [](uint32_t v) { return v != 0; }, err, 4u) - 1;
+    const uint32_t sz =
+        (SC_WPRE && vpre ? vpre : sc_wait(&S.rsize[slot], [](uint32_t v) { return v != 0; }, err, 4u)) - 1;
     STAMP(8)
     if (err) break;
+    if (SC_WPRE)
+      vpre = k + 1 < k1 ? uniform(__hip_atomic_load(&S.rsize[(k + 1) % kScRing], __ATOMIC_ACQUIRE,
+                                                    __HIP_MEMORY_SCOPE_WORKGROUP))
+                        : 0u;
     if (!(SC_ABL & 32)) sc_copy_out(dst + o, S.ring[slot], sz, lane);
     STAMP(9)
     o += sz;
