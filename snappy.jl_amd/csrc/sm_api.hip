@@ -99,6 +99,10 @@ struct sm_ctx {
   std::mutex mu;       // serialises the host-buffer entry points (they share the scratch above)
 };
 
+#ifndef SM_SMALL_BODY8  // path 4 when the body is at most SM_SMALL_BODY8/8 of the output
+#define SM_SMALL_BODY8 8
+#endif
+
 namespace {
 
 bool valid_mode(int m) { return m == SM_MODE_REFERENCE || m == SM_MODE_FAST || m == SM_MODE_FAST_DENSE; }
@@ -1029,10 +1033,13 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   // and this library all write such streams); otherwise, or on any error, the in-order decode
   size_t hdr = 0;
   (void)sm_parse32((const uint8_t*)compressed, n, 0, &size, &hdr);
-  // (a body nearly as long as its output is mostly literals, which the in-order engine copies
-  // HBM to HBM at bandwidth: path 0 is faster there)
+  // (a body longer than its output is all literals, which the in-order engine copies HBM to HBM at
+  // bandwidth: path 0 is faster there -- fireworks.jpeg 59 us against ~100; a body just under
+  // its output is random data with short copies sprinkled in, which path 0 walks in small batches
+  // of one wave: alice29.snappy's fast stream 573 us there, 114 us in path 4, so path 4 takes
+  // everything up to body == output; round 4's bound was 7/8)
   if (ctx->small && size >= kSmallMinOutput && size <= kSmallMaxOutput && n > hdr &&
-      (uint64_t)(n - hdr) * 8 <= (uint64_t)size * 7 &&
+      (uint64_t)(n - hdr) * 8 <= (uint64_t)size * SM_SMALL_BODY8 &&
       (n - hdr + sm::kSmallChunk - 1) / sm::kSmallChunk <= kSmallMaxChunks) {
     const int r = small_uncompress(ctx, (uint32_t)n, (uint32_t)hdr, size, (uint8_t*)uncompressed);
     if (r < 0) return SM_ERR_DEVICE;

@@ -502,11 +502,11 @@ def _big_corpus(n):
 def small_path(sm, comp):
     """Whether sm_uncompress takes path 4 (small stream on the device, sm_api.hip
     small_uncompress) for this stream: 4 KiB..64 MiB of output from a body of <= 1024 index
-    chunks of 1 KiB (1 MiB) and at most 7/8 of the output (else mostly literals: path 0)."""
+    chunks of 1 KiB (1 MiB) and at most as long as the output (else all literals: path 0)."""
     size, hdr = sm.parse32(comp, 0)
     body = len(comp) - hdr
     return (4096 <= size <= (64 << 20) and body > 0 and (body + 1023) // 1024 <= 1024
-            and body * 8 <= size * 7)
+            and body <= size)
 
 
 def test_uncompress_large_stream_parallel(sm, oracle, libsnappy, gpu_available):
