@@ -389,7 +389,7 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   const uint32_t nchunks = (n - ip0 + kSmallChunk - 1) / kSmallChunk;
   uint32_t rounds = 1;  // kSmallHops^rounds >= size: every chain (at most size steps) resolves
   for (uint64_t reach = sm::kSmallHops; reach < size; reach *= sm::kSmallHops) ++rounds;
-  const size_t path_off = align_up((size_t)nchunks * kIdxEntries * 8 + (size_t)nchunks * sm::kDeepLevels * 16, 256);  // records, deep records
+  const size_t path_off = align_up((size_t)nchunks * kIdxEntries * 8 + (size_t)nchunks * sm::kDeepChains * sm::kDeepLevels * 16, 256);  // records, deep records
   const size_t ctl_off = align_up(path_off + (size_t)nchunks * sizeof(sm::OriginPath), 256);
   const size_t ctl_n = 4 + rounds;
   if (ctx->idx.ensure(ctl_off + ctl_n * 4) != hipSuccess) return 0;

@@ -856,12 +856,13 @@ __device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint
   produced = o;
 }
 
-// kDeep (path 4): also deep[kDeepLevels c] = (x, exit, output, 1) for entering the chunk where
-// lane 0's path leaves this one, x, when x lies kIdxEntries or more bytes into it (a long literal
-// across the boundary): the entry the device chain needs there whenever its walk merged with
-// lane 0's path here (then its exit is x).  Level k + 1 likewise enters where level k's walk
-// leaves (consecutive long literals: the chunks between start inside a literal, and their own
-// lane-0 paths need not be the stream's).  .w = 0: no such level.
+// kDeep (path 4): also deep[kDeepLevels (kDeepChains c + ch)] = (x, exit, output, 1) for entering
+// the chunk where this one's entry walks leave it, x, when x lies kIdxEntries or more bytes into
+// it (a long literal across the boundary): the entry the device chain needs there whenever its
+// walk passed through this chunk from one of the entries (chain 0: lane 0's exit, chains 1..:
+// other distinct entry exits).  Level k + 1 likewise enters where level k's walk leaves
+// (consecutive long literals: the chunks between start inside a literal, and their own lane-0
+// paths need not be the stream's).  .w = 0: no such level.
 template <uint32_t kC, bool kDeep>  // compressed bytes per chunk (kIdxChunk; path 4: kSmallChunk)
 __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
                                                      uint2* rec, uint4* deep) {
@@ -980,22 +981,42 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
   // (exit, output) pairs side by side: the host's walk over the records reads one cache line
   rec[c * kIdxEntries + lane] = make_uint2((uint32_t)min(ex, (uint64_t)0xffffffffu), res);
   if constexpr (kDeep) {
-    uint64_t x = exit0;
-    for (uint32_t k = 0; k < kDeepLevels; ++k) {
-      const uint64_t dl = (x - ip0) / kC, db = ip0 + dl * kC;
-      uint4 dr = make_uint4(0, 0, 0, 0);
-      if (x < (uint64_t)N - 1 && x - db >= kIdxEntries) {
-        uint64_t dex, dot;
-        dev_walk(in, N, x, min(db + kC, (uint64_t)N - 1), jt, lane, buf, dex, dot);  // (buf: free now)
-        dr = make_uint4((uint32_t)x, (uint32_t)min(dex, (uint64_t)0xffffffffu),
-                        (uint32_t)min(dot, (uint64_t)0xffffffffu), 1u);
-        x = dex;
+    // chain 0 starts at lane 0's exit; chains 1.. at other distinct exits of the entry lanes that
+    // land kIdxEntries or more bytes into a chunk (the records there do not cover them: a walk
+    // that did not meet lane 0's path, e.g. one inside a long literal).  tools/chain_model.py
+    // --distinct: paper-100k.pdf's fast stream 19 chain walks with one chain, 7 with four.
+    auto deep_at = [&](uint64_t v) {
+      const uint64_t db = ip0 + ((v - ip0) / kC) * kC;
+      return v < (uint64_t)N - 1 && v - db >= kIdxEntries;
+    };
+    const uint32_t ex32 = (uint32_t)min(ex, (uint64_t)0xffffffffu);
+    uint64_t more = ballot(ex != exit0 && deep_at(ex));
+    uint64_t x0 = exit0;
+    for (uint32_t ch = 0; ch < kDeepChains; ++ch) {
+      uint64_t x = ~0ull;  // (no chain: zero records)
+      if (ch == 0) {
+        x = x0;
+      } else if (more) {
+        x = readlane(ex32, ctz64(more));
+        more &= ballot(ex32 != (uint32_t)x);
       }
-      if (lane == 0) deep[kDeepLevels * c + k] = dr;
-      if (!dr.w) {
-        for (uint32_t j = k + 1; j < kDeepLevels; ++j)
-          if (lane == 0) deep[kDeepLevels * c + j] = make_uint4(0, 0, 0, 0);
-        break;
+      uint4* const dc = deep + (size_t)(kDeepChains * c + ch) * kDeepLevels;
+      for (uint32_t k = 0; k < kDeepLevels; ++k) {
+        uint4 dr = make_uint4(0, 0, 0, 0);
+        if (x != ~0ull && deep_at(x)) {
+          const uint64_t db = ip0 + ((x - ip0) / kC) * kC;
+          uint64_t dex, dot;
+          dev_walk(in, N, x, min(db + kC, (uint64_t)N - 1), jt, lane, buf, dex, dot);  // (buf: free now)
+          dr = make_uint4((uint32_t)x, (uint32_t)min(dex, (uint64_t)0xffffffffu),
+                          (uint32_t)min(dot, (uint64_t)0xffffffffu), 1u);
+          x = dex;
+        }
+        if (lane == 0) dc[k] = dr;
+        if (!dr.w) {
+          for (uint32_t j = k + 1; j < kDeepLevels; ++j)
+            if (lane == 0) dc[j] = make_uint4(0, 0, 0, 0);
+          break;
+        }
       }
     }
   }
@@ -1341,9 +1362,9 @@ __global__ __launch_bounds__(64) void k_stream_chain(const uint8_t* __restrict__
         nsrc = dsrc;
         nlev = dlev + 1;
       }
-      if (!(dr.w && dr.x == y) && cprev != 0xffffffffu) {
-        dr = get(kDeepLevels * cprev);
-        nsrc = cprev;
+      for (uint32_t ch = 0; ch < kDeepChains && !(dr.w && dr.x == y) && cprev != 0xffffffffu; ++ch) {
+        dr = get(kDeepLevels * (kDeepChains * cprev + ch));
+        nsrc = kDeepChains * cprev + ch;
         nlev = 0;
       }
       if (dr.w && dr.x == y) {
@@ -1509,7 +1530,7 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
                                uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
                                uint8_t* out, uint32_t* words, hipStream_t s) {
   if (nchunks == 0 || size == 0 || rounds == 0 || 4 + rounds > kWave) return hipErrorInvalidValue;
-  uint4* deep = reinterpret_cast<uint4*>(rec + (size_t)nchunks * kIdxEntries * 2);  // kDeepLevels per chunk
+  uint4* deep = reinterpret_cast<uint4*>(rec + (size_t)nchunks * kIdxEntries * 2);  // kDeepChains x kDeepLevels per chunk
   hipLaunchKernelGGL((k_stream_index<kSmallChunk, true>), dim3(nchunks), dim3(64), 0, s, in, N, ip0,
                      reinterpret_cast<uint2*>(rec), deep);
   hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(64), 0, s, in, N, ip0, size, nchunks,

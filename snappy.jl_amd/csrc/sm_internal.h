@@ -55,7 +55,8 @@ constexpr uint32_t kIdxChunk = 4096;  // compressed bytes per index chunk
 constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
 constexpr uint32_t kSmallChunk = 1024;  // path 4 (a small stream on the device): bytes per index chunk
 constexpr uint32_t kSmallHops = 64;     // path 4: chain steps per pointer per resolve launch
-constexpr uint32_t kDeepLevels = 4;     // path 4: deep-entry records per chunk (consecutive long literals)
+constexpr uint32_t kDeepLevels = 4;     // path 4: deep-entry records per chain (consecutive long literals)
+constexpr uint32_t kDeepChains = 4;     // path 4: deep-record chains per chunk (distinct entry-lane exits)
 constexpr uint32_t kIdxPad = 288;     // staged bytes past a chunk: +16 entry slack, a 256-byte walk window + 16
 struct StreamFrag {
   uint32_t y;    // a true tag start at or before the fragment's first tag (chunk entry)
@@ -86,8 +87,8 @@ hipError_t launch_path_check(const uint8_t* in, uint32_t N, uint32_t size, const
                              int32_t* status, hipStream_t s);
 hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, hipStream_t s);
 // A small stream entirely on the device (index, chain, fill, `rounds` resolve launches, gather; no
-// host synchronisation).  rec: nchunks * kIdxEntries u32 pairs, then nchunks * kDeepLevels
-// 16-byte deep-entry records; path: nchunks elements; ctl: 4 +
+// host synchronisation).  rec: nchunks * kIdxEntries u32 pairs, then nchunks * kDeepChains *
+// kDeepLevels 16-byte deep-entry records; path: nchunks elements; ctl: 4 +
 // rounds u32 (zeroed by the chain kernel) -- ctl[0] path elements, ctl[1] != 0: the chain found no exact path (fall
 // back), ctl[2] != 0: an element failed its checks (fall back), ctl[4 + r] != 0: pointers still
 // unresolved after round r.  P: size u32.  The resolve launches write the output (each quad of

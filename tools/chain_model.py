@@ -50,24 +50,33 @@ def walk(b, p, lim):
     return p, o
 
 
-def model(b, levels):
+def model(b, levels, distinct=1):
+    """distinct: deep records for up to that many distinct exits of the chunk's 64 entry lanes
+    (1: lane 0's exit only, the kernel as built)."""
     N = len(b)
     size, ip0 = varint(b)
     nch = (N - ip0 + KC - 1) // KC
-    deep = []
+    deep = []   # per chunk: a list of record chains, each a list of (x, exit) levels
     for c in range(nch):
         s = ip0 + c * KC
-        x, _ = walk(b, s, min(s + KC, N - 1))
-        lv = []
-        for _ in range(levels):
-            dl = (x - ip0) // KC
-            db = ip0 + dl * KC
-            if not (x < N - 1 and x - db >= ENTRIES):
-                break
-            dex, _ = walk(b, x, min(db + KC, N - 1))
-            lv.append((x, dex))
-            x = dex
-        deep.append(lv)
+        exits = []
+        for l in range(ENTRIES if distinct > 1 else 1):
+            x, _ = walk(b, s + l, min(s + KC, N - 1))
+            if x not in exits:
+                exits.append(x)
+        chains = []
+        for x in exits[:distinct]:
+            lv = []
+            for _ in range(levels):
+                dl = (x - ip0) // KC
+                db = ip0 + dl * KC
+                if not (x < N - 1 and x - db >= ENTRIES):
+                    break
+                dex, _ = walk(b, x, min(db + KC, N - 1))
+                lv.append((x, dex))
+                x = dex
+            chains.append(lv)
+        deep.append(chains)
     y, n_rec, n_deep, n_walk = ip0, 0, 0, 0
     cprev, dsrc, dlev = None, None, 0
     walk_bytes = 0
@@ -81,10 +90,13 @@ def model(b, levels):
             dsrc = None
         else:
             hit = None
-            if dsrc is not None and dlev + 1 < len(deep[dsrc]) and deep[dsrc][dlev + 1][0] == y:
+            if dsrc is not None and dlev + 1 < len(deep[dsrc[0]][dsrc[1]]) and deep[dsrc[0]][dsrc[1]][dlev + 1][0] == y:
                 hit = (dsrc, dlev + 1)
-            elif cprev is not None and deep[cprev] and deep[cprev][0][0] == y:
-                hit = (cprev, 0)
+            elif cprev is not None:
+                for i, ch in enumerate(deep[cprev]):
+                    if ch and ch[0][0] == y:
+                        hit = ((cprev, i), 0)
+                        break
             ex, _ = walk(b, y, min(base + KC, N - 1))
             if hit:
                 n_deep += 1
@@ -102,11 +114,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("streams", nargs="+")
     ap.add_argument("--levels", type=int, default=4)
+    ap.add_argument("--distinct", type=int, default=1, help="deep-record chains per chunk (distinct entry exits)")
     a = ap.parse_args()
     print("%-40s %6s %6s %6s %6s %8s" % ("stream", "chunks", "rec", "deep", "walks", "walk B"))
     for f in a.streams:
         b = open(f, "rb").read()
-        print("%-40s %6d %6d %6d %6d %8d" % ((f.split("/")[-1],) + model(b, a.levels)))
+        print("%-40s %6d %6d %6d %6d %8d" % ((f.split("/")[-1],) + model(b, a.levels, a.distinct)))
 
 
 if __name__ == "__main__":
