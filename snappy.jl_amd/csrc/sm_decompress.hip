@@ -989,8 +989,11 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
       const uint64_t db = ip0 + ((v - ip0) / kC) * kC;
       return v < (uint64_t)N - 1 && v - db >= kIdxEntries;
     };
+    // (only exits inside the next chunk: the entry lanes that are not on the stream's path read
+    // garbage as tags and often jump far -- chains for those cost alice29.txt 10 us, and the
+    // model finds the same 7 walks on paper-100k.pdf without them)
     const uint32_t ex32 = (uint32_t)min(ex, (uint64_t)0xffffffffu);
-    uint64_t more = ballot(ex != exit0 && deep_at(ex));
+    uint64_t more = ballot(ex != exit0 && ex < (uint64_t)s + 2 * kC && deep_at(ex));
     uint64_t x0 = exit0;
     for (uint32_t ch = 0; ch < kDeepChains; ++ch) {
       uint64_t x = ~0ull;  // (no chain: zero records)

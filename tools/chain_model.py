@@ -5,6 +5,7 @@ Streams from tools/dump_streams.py (gpurun_out/streams/)."""
 import argparse
 
 KC = 1024        # kSmallChunk
+NEXTONLY = False  # extra chains only for exits inside the next chunk
 ENTRIES = 64     # kIdxEntries
 
 
@@ -62,6 +63,8 @@ def model(b, levels, distinct=1):
         exits = []
         for l in range(ENTRIES if distinct > 1 else 1):
             x, _ = walk(b, s + l, min(s + KC, N - 1))
+            if l and NEXTONLY and not (x < s + 2 * KC):
+                continue  # (an entry lane's exit past the next chunk: not used)
             if x not in exits:
                 exits.append(x)
         chains = []
@@ -115,7 +118,10 @@ def main():
     ap.add_argument("streams", nargs="+")
     ap.add_argument("--levels", type=int, default=4)
     ap.add_argument("--distinct", type=int, default=1, help="deep-record chains per chunk (distinct entry exits)")
+    ap.add_argument("--next-only", action="store_true", help="extra chains only for exits inside the next chunk")
     a = ap.parse_args()
+    global NEXTONLY
+    NEXTONLY = a.next_only
     print("%-40s %6s %6s %6s %6s %8s" % ("stream", "chunks", "rec", "deep", "walks", "walk B"))
     for f in a.streams:
         b = open(f, "rb").read()
