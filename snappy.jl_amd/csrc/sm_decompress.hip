@@ -58,8 +58,8 @@ constexpr uint32_t kRingMirror = 96;  // the ring's first bytes again past its e
                                       // 16-byte pieces (<= 64 B) read at ring offset + 48 + 20
 constexpr uint32_t kMaxBatchLit = 200;  // longer literals stop a window walk (size 255)
 constexpr int kWalkLevels = 5;  // tables J0..J4 in LDS; J5 (bit 5 of a lane's chain index) = J4 o J4
-constexpr int kJtRow = 264;             // a jump-table row (u16): positions 0..255, then 256 = beyond the window
-constexpr int kJt = kWalkLevels * kJtRow;  // u16 jump-table entries of a walk
+constexpr int kJtRow = 256;             // a jump-table row (u8): positions 0..254, 255 = beyond the window
+constexpr int kJt = kWalkLevels * kJtRow / 2;  // u16 words of a walk's jump tables (1.25 KB)
 __device__ inline uint32_t load_word(const uint8_t* __restrict__ in, uint32_t N, uint32_t p) {
   if (p + 3 < N && (((uintptr_t)(in + p)) & 3) == 0) return *reinterpret_cast<const uint32_t*>(in + p);
   uint32_t v = 0;
@@ -237,37 +237,36 @@ __device__ inline void win_flush(uint8_t* out, const uint8_t* win, uint32_t wbas
   if (lane < to - from) out[from + lane] = win[from + lane - wbase];
 }
 
-// Tag walk over a 256-byte window by pointer doubling (VALU + LDS, no serial loop).
-// cw = the 8 stream bytes at window position 4*lane; rlim (<= 256) = the parse limit relative
-// to the window (window end or N-1, internal.jl:416).  Every lane computes the speculative
-// sizes of its 4 positions (packed u8 in `sizes`, 255 = a literal too long for a batch).
-// J0[p] = p + size(p), clamped to 256 (beyond the window; its row entry maps to itself, so no
-// read is conditional); a long literal is a stop node (J0[p] = p).  Positions at or after rlim
-// need no stops: a chain's positions increase, so the tags before rlim are a prefix of lanes
-// and the final count drops the rest.
-// J_k = J_{k-1} o J_{k-1}, k < 5, in LDS (J5 = J4 o J4 is applied as two J4 reads, which
-// keeps the decoder's LDS at 7.7 KB: 20 waves per CU): 64 tags = chain elements 0..63.
-// Lane t then holds tag t directly -- J_k applied for every set bit k of t -- with its window
-// position cpos and size csz; stop nodes are fixed points, so the tags are a prefix of
-// lanes.  Returns their count.
-__device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt, uint32_t lane, uint32_t& cpos,
+// Tag walk over a 255-byte window by pointer doubling (VALU + LDS, no serial loop).
+// cw = the 8 stream bytes at window position 4*lane; rlim = the parse limit relative to the
+// window (window end or N-1, internal.jl:416), clamped to 255.  Every lane computes the
+// speculative sizes of its 4 positions (packed u8 in `sizes`, 255 = a literal too long for a
+// batch).  J0[p] = p + size(p), clamped to 255 (beyond the window: position 255 is never a tag
+// of this window, and its entry maps to itself, so no read is conditional); a long literal is a
+// stop node (J0[p] = p).  Positions at or after rlim need no stops: a chain's positions increase,
+// so the tags before rlim are a prefix of lanes and the final count drops the rest.
+// J_k = J_{k-1} o J_{k-1}, k < 5, in LDS as u8 rows (positions are bytes: a read's address is the
+// row base plus the value, and five rows take 1.25 KB), J5 = J4 o J4 applied as two J4 reads:
+// 64 tags = chain elements 0..63.  Lane t then holds tag t directly -- J_k applied for every set
+// bit k of t -- with its window position cpos and size csz; stop nodes are fixed points, so the
+// tags are a prefix of lanes.  Returns their count.
+__device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt16, uint32_t lane, uint32_t& cpos,
                                        uint32_t& csz, uint32_t& sizes) {
+  uint8_t* const jt = reinterpret_cast<uint8_t*>(jt16);
+  rlim = min(rlim, 255u);
   sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
-  // (the rows hold byte offsets into a row, 2 x position: a read's address is the row base plus
-  // the value, no shift per read)
-  const uint8_t* const jb = reinterpret_cast<const uint8_t*>(jt);
-  auto rd = [&](int k, uint32_t x2) -> uint32_t {
-    return *reinterpret_cast<const uint16_t*>(jb + 2 * k * kJtRow + x2);
+  auto rd = [&](int k, uint32_t x) -> uint32_t { return jt[k * kJtRow + x]; };
+  auto row = [&](int k, const uint32_t (&J)[4]) {
+    *reinterpret_cast<uint32_t*>(jt + k * kJtRow + 4 * lane) = J[0] | (J[1] << 8) | (J[2] << 16) | (J[3] << 24);
   };
   uint32_t J[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const uint32_t p = 4 * lane + j;
     const uint32_t sz = (sizes >> (8 * j)) & 0xff;
-    J[j] = 2 * (sz == 255 ? p : min(p + sz, 256u));  // 256: beyond the window
+    J[j] = sz == 255 ? p : min(p + sz, 255u);  // 255: beyond the window
   }
-  if (lane < kWalkLevels) jt[lane * kJtRow + 256] = 512;  // every row maps 256 to itself
-  *reinterpret_cast<uint2*>(jt + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+  row(0, J);
   // The J_k are powers of J0, so they commute: lane t applies J_k for bit k of t as soon as row k
   // is built, its read issued with the next row's reads (the chain does not wait for every row)
   uint32_t c = 0;
@@ -278,9 +277,9 @@ __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt,
 #pragma unroll
     for (int j = 0; j < 4; ++j) J[j] = rd(k - 1, J[j]);
     c = ((lane >> (k - 1)) & 1u) ? t : c;
-    *reinterpret_cast<uint2*>(jt + k * kJtRow + 4 * lane) = make_uint2(J[0] | (J[1] << 16), J[2] | (J[3] << 16));
+    row(k, J);
   }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the u16 reads below follow the uint2 stores
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the u8 reads below follow the row stores
   {
     const uint32_t t = rd(kWalkLevels - 1, c);
     c = ((lane >> (kWalkLevels - 1)) & 1u) ? t : c;
@@ -289,10 +288,9 @@ __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt,
     c = rd(kWalkLevels - 1, c);
     c = rd(kWalkLevels - 1, c);
   }
-  c >>= 1;  // (a position again)
   // (the shuffle runs with every lane active: a ds_bpermute from an inactive lane reads 0)
   const uint32_t szw = __shfl(sizes, (c >> 2) & 63u, 64);
-  const uint32_t sz = c < 256 ? (szw >> (8 * (c & 3))) & 0xffu : 0u;
+  const uint32_t sz = (szw >> (8 * (c & 3))) & 0xffu;
   cpos = c;
   csz = sz;
   __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the next walk's stores follow these reads
