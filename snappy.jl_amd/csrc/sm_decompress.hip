@@ -146,7 +146,7 @@ __device__ inline void ring_fill(const uint8_t* __restrict__ in, uint32_t N, uin
 // before the window (only the last partial 16-byte block of a batch waits for the next flush,
 // and it is inside the window).  No position ever wraps: reads and writes are plain offsets.
 #ifndef SM_DEC_WIN
-#define SM_DEC_WIN 1792
+#define SM_DEC_WIN 2560
 #endif
 constexpr uint32_t kWin = SM_DEC_WIN;  // window bytes (a multiple of 16)
 #ifndef SM_DEC_BOUT
@@ -653,7 +653,7 @@ __device__ inline int32_t parse_header(const uint8_t* in, uint32_t N, uint32_t l
 }
 
 #ifndef SM_DEC_OCC
-#define SM_DEC_OCC 7  // waves per SIMD: 69 VGPRs, 5.6 KB LDS per wave
+#define SM_DEC_OCC 7  // waves per SIMD: 67 VGPRs, 5.0 KB LDS per wave (8: 64 VGPRs with a spill, 1.444 against 1.357 ms)
 #endif
 // one stream of the batch (block b) by one wave
 __device__ inline void decompress_block(const DecompressArgs& a, uint32_t b, uint8_t* sring, uint16_t* sjt, uint8_t* swin,
