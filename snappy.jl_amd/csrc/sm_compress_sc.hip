@@ -99,6 +99,9 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #ifndef SC_GC
 #define SC_GC 0
 #endif
+#ifndef SC_ORN  // 1: a literal piece ors only the dwords it reaches (2.049 -> 2.023 ms); 2: also its first
+#define SC_ORN 1  // dword and the copy tags' (per-dword branches: 2.063)
+#endif
 #ifndef SC_WPRE  // the writer reads the next slot's size word with this slot's bytes
 #define SC_WPRE 1
 #endif
@@ -280,10 +283,33 @@ __device__ inline void sc_lds_or(uint32_t a, uint4 v) {
                  : : "v"(wa), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4) : "memory");
 }
 
+// sc_lds_or for a piece of nb (1..16) bytes: the last three dwords only when the piece reaches
+// them (most literal runs are a few bytes: two ds_or_b32 instead of five)
+__device__ inline void sc_lds_orn(uint32_t a, uint4 v, uint32_t nb) {
+  if (!SC_ORN) return sc_lds_or(a, v);
+  const uint32_t wa = (a - 1u) & ~3u, t = 0u - a, d = a - wa;  // (d: 1..4, the piece starts in dword 0 or 1)
+  const uint32_t u0 = __builtin_amdgcn_alignbyte(v.x, 0u, t);
+  const uint32_t u1 = __builtin_amdgcn_alignbyte(v.y, v.x, t);
+  if (SC_ORN < 2 || d < 4) asm volatile("ds_or_b32 %0, %1" : : "v"(wa), "v"(u0) : "memory");
+  if (SC_ORN < 2 || d + nb > 4) asm volatile("ds_or_b32 %0, %1 offset:4" : : "v"(wa), "v"(u1) : "memory");
+  if (d + nb > 8) {
+    const uint32_t u2 = __builtin_amdgcn_alignbyte(v.z, v.y, t);
+    const uint32_t u3 = __builtin_amdgcn_alignbyte(v.w, v.z, t);
+    const uint32_t u4 = __builtin_amdgcn_alignbyte(0u, v.w, t);
+    asm volatile("ds_or_b32 %0, %1 offset:8\nds_or_b32 %0, %2 offset:12\nds_or_b32 %0, %3 offset:16"
+                 : : "v"(wa), "v"(u2), "v"(u3), "v"(u4) : "memory");
+  }
+}
+
 // ors the (up to 3) bytes of cv into the zeroed LDS byte array at byte address a
-__device__ inline void sc_lds_or3(uint32_t a, uint32_t cv) {
+__device__ inline void sc_lds_or3(uint32_t a, uint32_t cv, uint32_t cs = 3) {
   const uint32_t wa = (a - 1u) & ~3u, t = 0u - a;  // (as sc_lds_or)
   const uint32_t lo = __builtin_amdgcn_alignbyte(cv, 0u, t), hi = __builtin_amdgcn_alignbyte(0u, cv, t);
+  if (SC_ORN >= 2) {  // only the dwords the cs-byte tag reaches
+    if (a - wa < 4) asm volatile("ds_or_b32 %0, %1" : : "v"(wa), "v"(lo) : "memory");
+    if (a - wa + cs > 4) asm volatile("ds_or_b32 %0, %1 offset:4" : : "v"(wa), "v"(hi) : "memory");
+    return;
+  }
   asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
   if (SC_DUP & 32) asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
 }
@@ -803,12 +829,13 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
           uint4 v = sc_ld128(S.blk - 4, p + 3);  // bytes from position p - 1
           v.x = ts ? ((v.x & ~0xffu) | ((run - 1) << 2)) : v.x;
           // (lanes without a run write nothing: a shared dummy address serialises the atomics)
-          if (run) sc_lds_or(stga + at + ts - 1u, sc_trim1(v, run + 1));
+          if (run) sc_lds_orn(stga + at + ts - 1u, sc_trim1(v, run + 1), run + 1);
         }
         at += len;
         if (L <= 64) {
           uint32_t cs;
-          sc_lds_or3(stga + at, sc_copy_piece(off, L, cs));
+          const uint32_t cv = sc_copy_piece(off, L, cs);
+          sc_lds_or3(stga + at, cv, cs);
           at += cs;
         } else {  // emit_copy! (internal.jl:306-329): 64-byte pieces while >= 68, a 60 if > 64, the rest
           uint32_t R = L;
@@ -823,7 +850,8 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
             R -= 60;
           }
           uint32_t cs;
-          sc_lds_or3(stga + at, sc_copy_piece(off, R, cs));
+          const uint32_t cv = sc_copy_piece(off, R, cs);
+          sc_lds_or3(stga + at, cv, cs);
           at += cs;
         }
         p = q + L;
@@ -833,7 +861,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       const uint32_t run = ce - p;
       uint32_t tag = 0, ts = 0;
       if (!(tk.n == 0 && cont)) tag = sc_lit_tag(merged, ts);
-      sc_lds_or(stga + at, sc_trim(sc_prepend(sc_ld128(S.blk, p), tag, ts), min(ts + run, 16u)));
+      sc_lds_orn(stga + at, sc_trim(sc_prepend(sc_ld128(S.blk, p), tag, ts), min(ts + run, 16u)), min(ts + run, 16u));
       if (ts + run > 16) sc_lds_or(stga + at + 16, sc_trim(sc_ld128(S.blk, p + 16 - ts), ts + run - 16));
     }
   }
