@@ -404,16 +404,18 @@ def _decode_all(sm, streams):
 
 
 def test_decompress_window_boundaries(sm, oracle, gpu_available):
-    """Copies into long literals and across the LDS output window's reach (kLdsSrc =
-    kWin - kBatchOut - 64: 448 with the default 1 KiB window, 3008 with a 4 KiB one; nearer
-    sources are read from LDS, farther ones from HBM), overlapping copies after a long
-    literal, and batches whose output exceeds the batch cap."""
+    """Copies into long literals and across the LDS output window's reach (a linear window of
+    kWin = 2,560 bytes that keeps the last kKeep = 480+ bytes when it shifts: sources inside it
+    are read from LDS, older ones from HBM; round 4's ring reached 448), overlapping copies
+    (offset < 16 runs in the in-order tail) after a long literal, and batches whose output
+    exceeds the batch cap."""
     from streams import build
     rng = np.random.default_rng(3)
     big = rng.integers(0, 256, 5000, dtype=np.uint8).tobytes()
     cases = []
-    for off in (1, 2, 7, 8, 15, 16, 17, 64, 100, 446, 447, 448, 449, 450, 511, 512, 513, 959, 960, 961, 999,
-                1023, 1024, 1025, 2047, 2048, 3006, 3007, 3008, 3009, 3010, 4000, 4095, 4096, 4097, 4999, 5000):
+    for off in (1, 2, 7, 8, 15, 16, 17, 64, 100, 446, 447, 448, 449, 450, 479, 480, 481, 496, 511, 512, 513, 959,
+                960, 961, 999, 1023, 1024, 1025, 2047, 2048, 2558, 2559, 2560, 2561, 3006, 3007, 3008, 3009, 3010,
+                4000, 4095, 4096, 4097, 4999, 5000):
         for ln in (1, 4, 11, 12, 16, 33, 64):
             cases.append([("lit", big), ("copy", off, ln), ("copy", 3, 20), ("lit", b"xyz"), ("copy", off, ln)])
     mid = rng.integers(0, 256, 150, dtype=np.uint8).tobytes()  # a 65..200-byte literal
