@@ -379,7 +379,7 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
 #define SM_SMALL_MIN 4096
 #endif
 constexpr uint32_t kSmallMinOutput = SM_SMALL_MIN;  // smaller streams: the one-wave decode
-constexpr uint32_t kSmallMaxChunks = 1024;         // compressed bodies up to 1 MiB
+constexpr uint32_t kSmallMaxChunks = (1u << 20) / sm::kSmallChunk;  // compressed bodies up to 1 MiB
 constexpr uint32_t kSmallMaxOutput = 64u << 20;    // 4 B of origin pointer per output byte
 constexpr uint32_t kPinnedOutMax = 16u << 20;      // outputs the last kernel writes into the pinned staging
 

@@ -53,7 +53,10 @@ hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 // compressed body, then one wave per 64 KiB output fragment (see sm_decompress.hip).
 constexpr uint32_t kIdxChunk = 4096;  // compressed bytes per index chunk
 constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
-constexpr uint32_t kSmallChunk = 1024;  // path 4 (a small stream on the device): bytes per index chunk
+#ifndef SM_SMALL_CHUNK
+#define SM_SMALL_CHUNK 1024
+#endif
+constexpr uint32_t kSmallChunk = SM_SMALL_CHUNK;  // path 4 (a small stream on the device): bytes per index chunk
 constexpr uint32_t kSmallHops = 64;     // path 4: chain steps per pointer per resolve launch
 constexpr uint32_t kDeepLevels = 4;     // path 4: deep-entry records per chain (consecutive long literals)
 constexpr uint32_t kDeepChains = 4;     // path 4: deep-record chains per chunk (distinct entry-lane exits)
