@@ -759,25 +759,32 @@ __device__ inline void stage_bytes(uint8_t* buf, const uint8_t* __restrict__ in,
                                    uint32_t lane) {
   // dword k = stream bytes [s+4k, s+4k+4): two aligned global dwords + v_alignbyte, all of a
   // lane's loads issued before its LDS stores (len % 256 == 0 words per lane is not assumed)
+  // Branch-free, so that every load is in flight at once (loads under divergent branches get a
+  // wait at each join: six serial round trips per stage).  Aligned dwords are clamped to the one
+  // holding byte N - 1 (the aligned dword at in + s - mis shares in[s]'s page), and the bytes at
+  // or past N are masked to zero.
   constexpr int kU = 6;
+  uint32_t* dst = reinterpret_cast<uint32_t*>(buf);
+  const uint32_t nw = (len + 3) / 4;
+  if (N == 0) {
+    for (uint32_t k = lane; k < nw; k += kWave) dst[k] = 0;
+    return;
+  }
   const uint32_t mis = (uint32_t)((uintptr_t)(in + s) & 3u);
   const uint32_t* src = reinterpret_cast<const uint32_t*>(in + s - mis);
-  const uint32_t nw = (len + 3) / 4;
-  uint32_t* dst = reinterpret_cast<uint32_t*>(buf);
+  const int64_t klast = ((intptr_t)((uintptr_t)(in + N - 1) & ~(uintptr_t)3) - (intptr_t)src) / 4;  // (< 0: s >= N)
   for (uint32_t k0 = lane; k0 < nw; k0 += kU * kWave) {
     uint32_t w[kU];
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const uint32_t k = k0 + u * kWave;
-      const uint64_t b = (uint64_t)s + 4 * k;  // stream offset of word k
-      if (k < nw && s >= mis && b - mis + 8 <= N) {
-        w[u] = __builtin_amdgcn_alignbyte(src[k + 1], src[k], mis);
-      } else {
-        uint32_t v = 0;
-        if (k < nw)
-          for (uint32_t j = 0; j < 4; ++j) v |= (b + j < N ? (uint32_t)in[b + j] : 0u) << (8 * j);
-        w[u] = v;
-      }
+      const int64_t k = k0 + u * kWave;
+      w[u] = __builtin_amdgcn_alignbyte(src[min(k + 1, klast)], src[min(k, klast)], mis);
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const uint64_t b = (uint64_t)s + 4 * (k0 + u * kWave);  // stream offset of word k
+      const uint64_t v = b < N ? (uint64_t)N - b : 0u;       // its bytes below N
+      w[u] &= v >= 4 ? 0xffffffffu : (uint32_t)((1ull << (8 * v)) - 1);
     }
 #pragma unroll
     for (int u = 0; u < kU; ++u)
@@ -1313,88 +1320,256 @@ __global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ 
 // launches and gathered -- one synchronisation for the whole call.  Any stream (no block
 // structure assumed); anything unexpected (an error, no progress, a length mismatch) is reported
 // in ctl[1] and the caller decodes the old way, which also finds the first error.
-constexpr uint32_t kChainLds = 256;  // chunks whose records the chain reads from LDS (128 KiB)
 constexpr uint32_t kFillStage = kSmallChunk + kIdxPad + 256;  // an element's tags and a window past them
+// The chain's LDS pool (u32 words): the entry records of the first chunks, compact (below), then
+// the deep records of as many chunks as still fit.  Everything else is read from HBM.
+constexpr uint32_t kChainThreads = 1024;  // all of them load the pool and take part in the runs
+constexpr uint32_t kChainPool = 96u * 1024 / 4;
+constexpr uint32_t kChainPath = 1024;  // path elements kept in LDS until the end (more: straight to HBM)
+constexpr uint32_t kDeepWords = kDeepChains * kDeepLevels * 4;  // a chunk's deep records
+constexpr uint32_t kRecNone = 0xffffffffu;                       // compact record: not representable
+constexpr uint32_t kChainNodes = kChainThreads;  // chunks the parallel runs cover, one thread each
+constexpr uint32_t kLift = 10;                   // 2^kLift >= kChainNodes: jump tables J[0..kLift)
+constexpr uint32_t kMinRun = 8;                  // links ahead that make a parallel run worth two barriers
+constexpr uint32_t kRunDone = 0xffffffffu;
+static_assert((1u << kLift) >= kChainNodes, "the jump tables must reach every node");
+// an entry record (exit, output) of chunk base `base`, compact: (output << 16) | (exit - base)
+__device__ inline uint32_t rec_compact(uint2 r, uint64_t base) {
+  const uint64_t d = (uint64_t)r.x - base;
+  return r.x >= base && d < 0xffffu && r.y <= 0xffffu ? (r.y << 16) | (uint32_t)d : kRecNone;
+}
 
+// The chain, in parallel where it can be.  Chunk c's lane-0 walk exits at E(c); entered anywhere,
+// its walk usually meets lane 0's path and exits there too.  The link c -> c' holds when E(c)
+// enters c' at an entry the records cover (offset < kIdxEntries) AND that entry's walk exits at
+// E(c') -- then the element after the one in c' is again decided by a link.  Pointer jumping over
+// the links (one thread per chunk, kLift rounds) gives every chunk its distance D to the end of
+// its links, the output SS on the way, and the jump tables J[k] (2^k links).  When the serial
+// chain (wave 0) stands on an entry whose walk exits at E(c1) with D(c1) >= kMinRun links ahead,
+// every chunk t tests in parallel whether it lies i = D(c1) - D(t) links along from c1 (J0 of the
+// node i - 1 along is t) and writes its own path element; wave 0 continues after the last.
+// Every run element is one the serial chain would take (same record, same exit), so the path is
+// identical; anything else (deep entries, walks, records not in LDS) stays serial.
 // ctl[0] = path elements, ctl[1] = 0 (the path covers exactly `size` bytes of output) or 1 (fall back)
-__global__ __launch_bounds__(64) void k_stream_chain(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
-                                                     uint32_t size, uint32_t nchunks, const uint2* __restrict__ rec,
-                                                     const uint4* __restrict__ deep, OriginPath* path, uint32_t* ctl,
-                                                     uint32_t nrounds) {
-  __shared__ uint2 srec[kChainLds * kIdxEntries];
+__global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
+                                                                uint32_t size, uint32_t nchunks,
+                                                                const uint2* __restrict__ rec,
+                                                                const uint4* __restrict__ deep, OriginPath* path,
+                                                                uint32_t* ctl, uint32_t nrounds) {
+  __shared__ __attribute__((aligned(16))) uint32_t pool[kChainPool];
+  __shared__ __attribute__((aligned(16))) OriginPath spath[kChainPath];
+  __shared__ uint16_t J[kLift][kChainNodes];
+  __shared__ uint32_t Dsh[kChainNodes], SSsh[kChainNodes], Esh[kChainNodes], Wsh[kChainNodes];
+  __shared__ uint32_t run[5];  // the run wave 0 asks for: c1 (kRunDone: finished), y, O, np, output of c1's element
   __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
   __shared__ __attribute__((aligned(16))) uint8_t stg[kDevWalkStage + 16];
-  const uint32_t lane = lane_id();
-  const bool inlds = nchunks <= kChainLds;
-  if (inlds) {  // (eight loads in flight per lane)
-    const uint32_t nr = nchunks * kIdxEntries;
-    for (uint32_t k0 = lane; k0 < nr; k0 += 8 * kWave) {
+  // one round trip for the whole pool: every thread's loads are in flight before its stores
+  const uint32_t nrec = min(nchunks, kChainPool / kIdxEntries);                    // chunks with LDS records
+  const uint32_t ndeep = min(nchunks, (kChainPool - nrec * kIdxEntries) / kDeepWords);  // ... and LDS deep records
+  uint32_t* const srec = pool;
+  uint4* const sdeep = reinterpret_cast<uint4*>(pool + nrec * kIdxEntries);  // (16-B aligned: nrec * 64 words)
+  const uint32_t t = threadIdx.x;
+  {  // (clamped indices, no branches around the loads: they all issue before the first wait)
+    const uint32_t nr = nrec * kIdxEntries, nd = ndeep * kDeepWords / 4;
+    for (uint32_t k0 = t; k0 < nr; k0 += 8 * kChainThreads) {
       uint2 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = k0 + u * kWave < nr ? rec[k0 + u * kWave] : make_uint2(0, 0);
+      for (int u = 0; u < 8; ++u) v[u] = rec[min(k0 + u * kChainThreads, nr - 1)];
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (k0 + u * kWave < nr) srec[k0 + u * kWave] = v[u];
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t k = k0 + u * kChainThreads;
+        if (k < nr) srec[k] = rec_compact(v[u], ip0 + (uint64_t)(k / kIdxEntries) * kSmallChunk);
+      }
+    }
+    for (uint32_t k0 = t; k0 < nd; k0 += 4 * kChainThreads) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = deep[min(k0 + u * kChainThreads, nd - 1)];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sdeep[min(k0 + u * kChainThreads, nd - 1)] = v[u];  // (past nd: the last again)
     }
   }
   __syncthreads();
+  const bool par = nchunks <= kChainNodes && nrec == nchunks;
+  if (par) {  // the links and their pointer jumping (a root links to itself)
+    uint32_t link = t, w = 0, e = 0xffffffffu;
+    if (t < nchunks) {
+      const uint32_t v0 = srec[t * kIdxEntries];
+      if (v0 != kRecNone) {
+        e = ip0 + t * kSmallChunk + (v0 & 0xffffu);
+        const uint32_t er = e - ip0, c2 = er / kSmallChunk, l2 = er % kSmallChunk;
+        if ((uint64_t)e < (uint64_t)N - 1 && l2 < kIdxEntries && c2 < nchunks && c2 > t) {
+          const uint32_t v2 = srec[c2 * kIdxEntries + l2], v20 = srec[c2 * kIdxEntries];
+          if (v2 != kRecNone && v20 != kRecNone && (v2 & 0xffffu) == (v20 & 0xffffu) && (v2 & 0xffffu) > l2) {
+            link = c2;
+            w = v2 >> 16;
+          }
+        }
+      }
+    }
+    Esh[t] = e;
+    Wsh[t] = w;
+    J[0][t] = (uint16_t)link;
+    uint32_t d = link != t ? 1u : 0u, ss = w, p = link;
+    Dsh[t] = d;
+    SSsh[t] = ss;
+    __syncthreads();
+    for (uint32_t r = 1; r <= kLift; ++r) {  // d, ss: over 2^r links; J[r] = J[r-1] o J[r-1]
+      const uint32_t dp = Dsh[p], sp = SSsh[p], pn = J[r - 1][p];
+      __syncthreads();
+      d += dp;
+      ss += sp;
+      Dsh[t] = d;
+      SSsh[t] = ss;
+      if (r < kLift) J[r][t] = (uint16_t)pn;
+      p = pn;
+      __syncthreads();
+    }
+  }
+  auto lift = [&](uint32_t x, uint32_t n) {
+#pragma unroll
+    for (uint32_t k = 0; k < kLift; ++k)
+      if ((n >> k) & 1u) x = J[k][x];
+    return x;
+  };
+  auto put = [&](uint32_t k, const OriginPath& pe) {
+    if (k < kChainPath)
+      spath[k] = pe;
+    else
+      path[k] = pe;
+  };
+  const uint32_t lane = lane_id();
+  const bool w0 = t < kWave;
   uint64_t y = ip0, O = 0;
   uint32_t np = 0, bad = 0, cprev = 0xffffffffu;  // the chunk of the previous element
   uint32_t dsrc = 0xffffffffu, dlev = 0;          // the deep record the previous element came from
-  while (y < (uint64_t)N - 1) {  // internal.jl:416
-    const uint32_t c = (uint32_t)((y - ip0) / kSmallChunk);
-    const uint64_t base = ip0 + (uint64_t)c * kSmallChunk, l = y - base;
-    uint64_t ex, ot;
-    if (l < kIdxEntries) {
-      const uint2 r = inlds ? srec[c * kIdxEntries + l] : rec[c * kIdxEntries + l];
-      ex = uniform(r.x);
-      ot = uniform(r.y);
-    } else {
-      // the next level of the deep record the previous element came from, else level 0 of the
-      // previous element's chunk (it left where that chunk's lane-0 path does), else a walk
-      auto get = [&](uint32_t i) {
-        const uint4 v = deep[i];
-        return make_uint4(uniform(v.x), uniform(v.y), uniform(v.z), uniform(v.w));
-      };
-      uint4 dr = make_uint4(0, 0, 0, 0);
-      uint32_t nsrc = 0xffffffffu, nlev = 0;
-      if (dsrc != 0xffffffffu && dlev + 1 < kDeepLevels) {
-        dr = get(kDeepLevels * dsrc + dlev + 1);
-        nsrc = dsrc;
-        nlev = dlev + 1;
+  while (true) {
+    if (w0) {
+      uint32_t c1 = kRunDone, out1 = 0;
+      while (y < (uint64_t)N - 1) {  // internal.jl:416
+        {  // the common step, an entry record in LDS, in a tight 32-bit loop (the general step below
+           // takes everything else, and re-checks what ended this loop)
+          uint32_t yr = (uint32_t)(y - ip0);
+          bool stop = false;
+          while (true) {
+            const uint32_t c = yr / kSmallChunk, l = yr % kSmallChunk;
+            if (l >= kIdxEntries || c >= nrec) break;
+            const uint32_t v = uniform(srec[c * kIdxEntries + l]), d = v & 0xffffu;
+            if (v == kRecNone || d <= l || np >= nchunks) break;
+            const uint32_t ot = v >> 16, exr = c * kSmallChunk + d, Oc = (uint32_t)O;  // (O <= size here)
+            if (par && uniform(Dsh[c]) >= kMinRun && ip0 + exr == uniform(Esh[c])) {  // a run from here
+              c1 = c;
+              out1 = ot;
+              break;
+            }
+            const OriginPath pe = {ip0 + yr, ip0 + exr, Oc, ot < 0xffffffffu - Oc ? ot : 0xffffffffu - Oc};
+            if (lane == 0) put(np, pe);
+            ++np;
+            O += ot;
+            cprev = c;
+            dsrc = 0xffffffffu;
+            yr = exr;
+            if (O > size || (uint64_t)ip0 + exr >= (uint64_t)N - 1) {
+              stop = true;
+              break;
+            }
+          }
+          y = ip0 + (uint64_t)yr;
+          if (stop || c1 != kRunDone) break;
+        }
+        const uint32_t c = (uint32_t)((y - ip0) / kSmallChunk);
+        const uint64_t base = ip0 + (uint64_t)c * kSmallChunk, l = y - base;
+        uint64_t ex, ot;
+        if (l < kIdxEntries) {
+          const uint32_t v = c < nrec ? srec[c * kIdxEntries + l] : kRecNone;
+          if (v != kRecNone) {
+            ex = base + (v & 0xffffu);
+            ot = v >> 16;
+          } else {
+            const uint2 r = rec[c * kIdxEntries + l];
+            ex = uniform(r.x);
+            ot = uniform(r.y);
+          }
+          dsrc = 0xffffffffu;
+        } else {
+          // candidates, one lane each, read at once: lane 0 the next level of the deep record the
+          // previous element came from, lanes 1..kDeepChains level 0 of the previous element's chunk's
+          // chains (it left where one of that chunk's entry walks does); the first that starts at y
+          // wins, else a walk
+          uint32_t idx = 0xffffffffu;
+          if (lane == 0 && dsrc != 0xffffffffu && dlev + 1 < kDeepLevels) idx = kDeepLevels * dsrc + dlev + 1;
+          if (lane >= 1 && lane <= kDeepChains && cprev != 0xffffffffu) idx = kDeepLevels * (kDeepChains * cprev + lane - 1);
+          uint4 dr = make_uint4(0, 0, 0, 0);
+          if (idx != 0xffffffffu) dr = idx < ndeep * kDeepChains * kDeepLevels ? sdeep[idx] : deep[idx];
+          const uint64_t hit = ballot(dr.w && dr.x == (uint32_t)y && y <= 0xffffffffull);
+          if (hit) {
+            const uint32_t h = ctz64(hit);
+            ex = readlane(dr.y, h);
+            ot = readlane(dr.z, h);
+            const uint32_t i = readlane(idx, h);
+            dsrc = i / kDeepLevels;
+            dlev = i % kDeepLevels;
+          } else {
+            dev_walk(in, N, y, min(base + kSmallChunk, (uint64_t)N - 1), jt, lane, stg, ex, ot);
+            dsrc = 0xffffffffu;
+          }
+        }
+        cprev = c;
+        if (np >= nchunks || ex <= y) {  // (never for a well-formed index: every element leaves its chunk)
+          bad = 1;
+          break;
+        }
+        {  // (into LDS: a global store per element made every step wait for the previous one's)
+          const uint32_t Oc = O < 0xffffffffull ? (uint32_t)O : 0xffffffffu;
+          const uint32_t e32 = ex < 0xffffffffull ? (uint32_t)ex : 0xffffffffu;
+          const uint32_t o32 = ot < (uint64_t)(0xffffffffu - Oc) ? (uint32_t)ot : 0xffffffffu - Oc;
+          if (lane == 0) put(np, {(uint32_t)y, e32, Oc, o32});
+        }
+        ++np;
+        O += ot;
+        y = ex;
+        if (O > size) break;
       }
-      for (uint32_t ch = 0; ch < kDeepChains && !(dr.w && dr.x == y) && cprev != 0xffffffffu; ++ch) {
-        dr = get(kDeepLevels * (kDeepChains * cprev + ch));
-        nsrc = kDeepChains * cprev + ch;
-        nlev = 0;
+      if (lane == 0) {
+        run[0] = c1;
+        run[1] = (uint32_t)y;
+        run[2] = (uint32_t)O;  // (O <= size when c1 is set)
+        run[3] = np;
+        run[4] = out1;
       }
-      if (dr.w && dr.x == y) {
-        ex = dr.y;
-        ot = dr.z;
-        dsrc = nsrc;
-        dlev = nlev;
-      } else {
-        dev_walk(in, N, y, min(base + kSmallChunk, (uint64_t)N - 1), jt, lane, stg, ex, ot);
+    }
+    __syncthreads();
+    const uint32_t c1 = run[0];
+    if (c1 == kRunDone) break;
+    {  // every chunk: is it i links along from c1?  Then its element is path element np + i.
+      const uint32_t y1 = run[1], O1 = run[2], np1 = run[3], out1 = run[4], D1 = Dsh[c1];
+      if (t < nchunks && t >= c1 && Dsh[t] <= D1) {
+        const uint32_t i = D1 - Dsh[t];
+        if (i == 0) {
+          if (t == c1) put(np1, {y1, Esh[c1], O1, out1});
+        } else {
+          const uint32_t p = lift(c1, i - 1);
+          if (J[0][p] == t && p != t) put(np1 + i, {Esh[p], Esh[t], O1 + out1 + SSsh[c1] - SSsh[p], Wsh[p]});
+        }
+      }
+      if (w0) {  // wave 0 goes on after the run's last element
+        const uint32_t root = lift(c1, D1);
+        np = np1 + D1 + 1;
+        O = (uint64_t)O1 + out1 + SSsh[c1];
+        y = Esh[root];
+        cprev = root;
         dsrc = 0xffffffffu;
+        if (O > size) {  // (the serial chain stops there too; the path is then rejected)
+          y = N;
+        }
       }
     }
-    if (l < kIdxEntries) dsrc = 0xffffffffu;
-    cprev = c;
-    if (np >= nchunks || ex <= y) {  // (never for a well-formed index: every element leaves its chunk)
-      bad = 1;
-      break;
-    }
-    if (lane == 0) {
-      const uint64_t Oc = min(O, (uint64_t)0xffffffffu);
-      path[np] = {(uint32_t)y, (uint32_t)min(ex, (uint64_t)0xffffffffu), (uint32_t)Oc,
-                  (uint32_t)min(ot, 0xffffffffull - Oc)};
-    }
-    ++np;
-    O += ot;
-    y = ex;
-    if (O > size) break;
+    __syncthreads();  // (run[] is rewritten next round; the run's LDS path elements are in place)
   }
+  if (!w0) return;
   if (O != size) bad = 1;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (lane 0's LDS stores before the copy's reads; the runs': barrier)
+  for (uint32_t k = lane; k < min(np, kChainPath); k += kWave) path[k] = spath[k];
   if (lane == 0) {
     ctl[0] = np;
     ctl[1] = bad;
@@ -1408,9 +1583,9 @@ __global__ __launch_bounds__(64) void k_origin_fill_dev(const uint8_t* __restric
                                                         uint32_t* ctl) {
   __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
   __shared__ __attribute__((aligned(16))) uint8_t buf[kFillStage + 16];
-  if (blockIdx.x >= uniform(__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ||
-      uniform(__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
-    return;
+  const uint32_t npath = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t fail = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (both in flight)
+  if (blockIdx.x >= uniform(npath) || uniform(fail)) return;
   const OriginPath pe = path[blockIdx.x];
   stage_bytes(buf, in, N, pe.y, kFillStage, lane_id());  // (zero past N, as load8z)
   __syncthreads();
@@ -1428,21 +1603,20 @@ __global__ __launch_bounds__(64) void k_origin_fill_dev(const uint8_t* __restric
 // the call's verdict words (ctl[1], ctl[2]); nothing else runs when the chain or a fill failed (P
 // is then not all written).  out and words may be device-mapped pinned host memory.
 constexpr uint32_t kHops = kSmallHops;
-__device__ inline bool small_failed(const uint32_t* ctl) {
-  return (__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
-          __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) != 0;
-}
 __global__ __launch_bounds__(256) void k_small_resolve(const uint8_t* __restrict__ in, uint32_t* P, uint32_t size,
                                                        uint32_t* ctl, uint32_t r, uint32_t last,
                                                        uint8_t* __restrict__ out, uint32_t* words) {
   uint32_t* const pend = ctl + 4;
   const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  // (the three control words in one round trip: later launches usually return here)
+  const uint32_t f1 = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t f2 = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t pprev = __hip_atomic_load(&pend[r > 0 ? r - 1 : 0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (r == 0 && t0 == 0) {
-    words[0] = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    words[1] = __hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    words[0] = f1;
+    words[1] = f2;
   }
-  if (small_failed(ctl)) return;
-  if (r > 0 && __hip_atomic_load(&pend[r - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+  if ((f1 | f2) != 0 || (r > 0 && pprev == 0)) return;
   uint32_t left = 0;
   for (uint32_t x = t0; x < size; x += gridDim.x * blockDim.x) {
     uint32_t v = P[x];
@@ -1450,8 +1624,15 @@ __global__ __launch_bounds__(256) void k_small_resolve(const uint8_t* __restrict
       if (r == 0) out[x] = in[v & 0x7fffffffu];  // (r > 0: written by an earlier launch)
       continue;
     }
+    // v < x: an earlier byte of the chain.  Every few hops the progress is published, so chains
+    // through x jump over it (any value a thread stores or reads is a point of the same chain, so
+    // stale or racing values are still correct): a run's chain then shrinks by doubling in
+    // practice, while kHops per launch bounds the work the round count assumes.
 #pragma unroll 1
-    for (uint32_t h = 0; h < kHops && !(v >> 31); ++h) v = P[v];  // v < x: an earlier byte of the chain
+    for (uint32_t h = 0; h < kHops && !(v >> 31); ++h) {
+      v = P[v];
+      if ((h & 3) == 3) P[x] = v;
+    }
     P[x] = v;
     if (v >> 31)
       out[x] = in[v & 0x7fffffffu];
@@ -1534,14 +1715,14 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
   uint4* deep = reinterpret_cast<uint4*>(rec + (size_t)nchunks * kIdxEntries * 2);  // kDeepChains x kDeepLevels per chunk
   hipLaunchKernelGGL((k_stream_index<kSmallChunk, true>), dim3(nchunks), dim3(64), 0, s, in, N, ip0,
                      reinterpret_cast<uint2*>(rec), deep);
-  hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(64), 0, s, in, N, ip0, size, nchunks,
+  hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(kChainThreads), 0, s, in, N, ip0, size, nchunks,
                      reinterpret_cast<const uint2*>(rec), deep, path, ctl, rounds);
   hipLaunchKernelGGL(k_origin_fill_dev, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
   // later launches usually find nothing pending and return at once: a small grid dispatches
   // faster, and strides over the pointers when some are left
   const uint32_t g1 = min(32768u, max(1u, (size + 255) / 256));
   for (uint32_t r = 0; r < rounds; ++r)
-    hipLaunchKernelGGL(k_small_resolve, dim3(r == 0 ? g1 : min(g1, 256u)), dim3(256), 0, s, in, P, size, ctl, r,
+    hipLaunchKernelGGL(k_small_resolve, dim3(r == 0 ? g1 : min(g1, 32u)), dim3(256), 0, s, in, P, size, ctl, r,
                        (uint32_t)(r + 1 == rounds), out, words);
   return hipGetLastError();
 }

@@ -57,7 +57,10 @@ constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
 #define SM_SMALL_CHUNK 1024
 #endif
 constexpr uint32_t kSmallChunk = SM_SMALL_CHUNK;  // path 4 (a small stream on the device): bytes per index chunk
-constexpr uint32_t kSmallHops = 64;     // path 4: chain steps per pointer per resolve launch
+#ifndef SM_SMALL_HOPS
+#define SM_SMALL_HOPS 1024
+#endif
+constexpr uint32_t kSmallHops = SM_SMALL_HOPS;  // path 4: chain steps per pointer per resolve launch
 constexpr uint32_t kDeepLevels = 4;     // path 4: deep-entry records per chain (consecutive long literals)
 constexpr uint32_t kDeepChains = 4;     // path 4: deep-record chains per chunk (distinct entry-lane exits)
 constexpr uint32_t kIdxPad = 288;     // staged bytes past a chunk: +16 entry slack, a 256-byte walk window + 16
