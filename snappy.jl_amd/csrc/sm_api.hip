@@ -380,13 +380,26 @@ int parallel_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t i
 #endif
 constexpr uint32_t kSmallMinOutput = SM_SMALL_MIN;  // smaller streams: the one-wave decode
 constexpr uint32_t kSmallMaxChunks = (1u << 20) / sm::kSmallChunk;  // compressed bodies up to 1 MiB
+// Index chunk size for path 4: 512-byte chunks halve the index and fill kernels' per-chunk walk
+// (both latency chains of 256-byte windows) but double the chain's elements and split more long
+// literals into deep entries.  Measured single calls (fast streams, r05): html (body 0.22 of the
+// output) 83 -> 70 us, alice29.txt (0.56) 82 -> 74, paper-100k.pdf (0.82, long literals) 145 ->
+// 184, urls.10K (0.48, 336 KB body) 150 -> 156.  So: fine chunks for bodies up to 0.6 of the
+// output and 256 KiB.
+#ifndef SM_SMALL_FINE_BODY10
+#define SM_SMALL_FINE_BODY10 6
+#endif
+uint32_t small_chunk(uint32_t body, uint32_t size) {
+  return (uint64_t)body * 10 <= (uint64_t)size * SM_SMALL_FINE_BODY10 && body <= (256u << 10) ? sm::kSmallChunkFine
+                                                                                               : sm::kSmallChunk;
+}
 constexpr uint32_t kSmallMaxOutput = 64u << 20;    // 4 B of origin pointer per output byte
 constexpr uint32_t kPinnedOutMax = 16u << 20;      // outputs the last kernel writes into the pinned staging
 
 int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8_t* host_out) {
   using sm::kIdxEntries;
-  using sm::kSmallChunk;
-  const uint32_t nchunks = (n - ip0 + kSmallChunk - 1) / kSmallChunk;
+  const uint32_t chunk = small_chunk(n - ip0, size);
+  const uint32_t nchunks = (n - ip0 + chunk - 1) / chunk;
   uint32_t rounds = 1;  // kSmallHops^rounds >= size: every chain (at most size steps) resolves
   for (uint64_t reach = sm::kSmallHops; reach < size; reach *= sm::kSmallHops) ++rounds;
   const size_t path_off = align_up((size_t)nchunks * kIdxEntries * 8 + (size_t)nchunks * sm::kDeepChains * sm::kDeepLevels * 16, 256);  // records, deep records
@@ -405,7 +418,7 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
   // the third verdict word is written by the device only when a pointer stays unresolved
   ((volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off))[2] = 0;
-  if (sm::launch_small_decode((const uint8_t*)ctx->in.p, n, ip0, size, nchunks, (uint32_t*)ib,
+  if (sm::launch_small_decode((const uint8_t*)ctx->in.p, n, ip0, size, chunk, nchunks, (uint32_t*)ib,
                               (sm::OriginPath*)(ib + path_off), d_ctl, (uint32_t*)ctx->org.p, rounds,
                               pin_out ? sdp : (uint8_t*)ctx->out.p, (uint32_t*)(sdp + w_off), s) != hipSuccess)
     return -1;

@@ -818,14 +818,15 @@ __device__ inline uint64_t load8z(const uint8_t* __restrict__ in, uint32_t N, ui
 // bytes [p, lim + 256 + 32) are staged in stg (LDS, kDevWalkStage bytes) first; a 256-byte
 // window of tags per step (walk_window, as k_origin_fill), a literal too long for a window by
 // itself (its far end read from HBM).
-constexpr uint32_t kDevWalkStage = kSmallChunk + kIdxPad;
+template <uint32_t kC>  // (the chunk size: lim - p <= kC)
 __device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint64_t p, uint64_t lim, uint16_t* jt,
                                 uint32_t lane, uint8_t* stg, uint64_t& exit_pos, uint64_t& produced) {
+  constexpr uint32_t kStage = kC + kIdxPad;
   const uint64_t sp = p;
-  stage_bytes(stg, in, N, (uint32_t)sp, kDevWalkStage, lane);
+  stage_bytes(stg, in, N, (uint32_t)sp, kStage, lane);
   __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: its LDS stores land before its loads)
   auto rd8 = [&](uint64_t x) -> uint64_t {
-    return x >= sp && x - sp + 8 <= kDevWalkStage ? lds_ld64(stg, (uint32_t)(x - sp)) : load8z(in, N, (uint32_t)x);
+    return x >= sp && x - sp + 8 <= kStage ? lds_ld64(stg, (uint32_t)(x - sp)) : load8z(in, N, (uint32_t)x);
   };
   uint64_t o = 0;
   while (p < lim) {
@@ -868,18 +869,26 @@ __device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint
 // other distinct entry exits).  Level k + 1 likewise enters where level k's walk leaves
 // (consecutive long literals: the chunks between start inside a literal, and their own lane-0
 // paths need not be the stream's).  .w = 0: no such level.
+// kDeep: one wave per deep-record chain (kDeepChains waves): wave 0 indexes the chunk, then each
+// wave walks its chain's levels (serial dev_walks) at the same time as the others.
+constexpr uint32_t index_threads(bool deep) { return deep ? kDeepChains * kWave : kWave; }
 template <uint32_t kC, bool kDeep>  // compressed bytes per chunk (kIdxChunk; path 4: kSmallChunk)
-__global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
-                                                     uint2* rec, uint4* deep) {
+__global__ __launch_bounds__(index_threads(kDeep)) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N,
+                                                                          uint32_t ip0, uint2* rec, uint4* deep) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kC + kIdxPad];
   __shared__ __attribute__((aligned(16))) uint16_t jt[6 * 256];  // walk tables, then the entry walk's 3 KiB
   __shared__ uint32_t bm[kC / 32];  // positions on lane 0's path
   __shared__ uint32_t cum[kC];      // output before each such position
-  const uint32_t c = blockIdx.x, lane = lane_id();
+  constexpr uint32_t kXw = kDeep ? kDeepChains - 1 : 1;  // waves 1.. : their own walk stage and tables
+  __shared__ __attribute__((aligned(16))) uint8_t xstg[kXw][kC + kIdxPad + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t xjt[kXw][kJt];
+  __shared__ uint64_t xs[kDeepChains];  // each chain's first entry (~0: none)
+  const uint32_t c = blockIdx.x, lane = lane_id(), wv = threadIdx.x / kWave;
   const uint32_t s = ip0 + c * kC;
+  if (wv == 0) {  // (one wave from here to the chain starts: LDS in order, signal fences only)
   stage_bytes(buf, in, N, s, kC + kIdxPad, lane);
   for (uint32_t k = lane; k < kC / 32; k += kWave) bm[k] = 0;
-  __syncthreads();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
   const uint64_t lim = min((uint64_t)s + kC, (uint64_t)N - 1);  // tags start below N-1 (:416)
   // lane 0's path: the tag walk from the chunk's first byte, a 256-byte window at a time
   uint64_t p = s, acc = 0, size, outb;
@@ -904,7 +913,7 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
     acc += readlane(excl + ob, ntok - 1);
     p = s + readlane(next, ntok - 1);
   }
-  __syncthreads();
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
   const uint64_t exit0 = p;
   const uint32_t tot0 = (uint32_t)acc;
   // Lanes 1..63 (entries at chunk bytes 1..63) walk until they meet lane 0's path or leave the
@@ -999,32 +1008,44 @@ __global__ __launch_bounds__(64) void k_stream_index(const uint8_t* __restrict__
     // model finds the same 7 walks on paper-100k.pdf without them)
     const uint32_t ex32 = (uint32_t)min(ex, (uint64_t)0xffffffffu);
     uint64_t more = ballot(ex != exit0 && ex < (uint64_t)s + 2 * kC && deep_at(ex));
-    uint64_t x0 = exit0;
     for (uint32_t ch = 0; ch < kDeepChains; ++ch) {
       uint64_t x = ~0ull;  // (no chain: zero records)
       if (ch == 0) {
-        x = x0;
+        x = exit0;
       } else if (more) {
         x = readlane(ex32, ctz64(more));
         more &= ballot(ex32 != (uint32_t)x);
       }
-      uint4* const dc = deep + (size_t)(kDeepChains * c + ch) * kDeepLevels;
-      for (uint32_t k = 0; k < kDeepLevels; ++k) {
-        uint4 dr = make_uint4(0, 0, 0, 0);
-        if (x != ~0ull && deep_at(x)) {
-          const uint64_t db = ip0 + ((x - ip0) / kC) * kC;
-          uint64_t dex, dot;
-          dev_walk(in, N, x, min(db + kC, (uint64_t)N - 1), jt, lane, buf, dex, dot);  // (buf: free now)
-          dr = make_uint4((uint32_t)x, (uint32_t)min(dex, (uint64_t)0xffffffffu),
-                          (uint32_t)min(dot, (uint64_t)0xffffffffu), 1u);
-          x = dex;
-        }
-        if (lane == 0) dc[k] = dr;
-        if (!dr.w) {
-          for (uint32_t j = k + 1; j < kDeepLevels; ++j)
-            if (lane == 0) dc[j] = make_uint4(0, 0, 0, 0);
-          break;
-        }
+      if (lane == 0) xs[ch] = x;
+    }
+  }
+  }  // (wave 0)
+  if constexpr (kDeep) {
+    __syncthreads();
+    const uint32_t ch = wv;
+    uint64_t x = xs[ch];
+    uint8_t* const stg = ch == 0 ? buf : xstg[ch - 1];  // (buf: free now)
+    uint16_t* const wjt = ch == 0 ? jt : xjt[ch - 1];
+    auto deep_at = [&](uint64_t v) {
+      const uint64_t db = ip0 + ((v - ip0) / kC) * kC;
+      return v < (uint64_t)N - 1 && v - db >= kIdxEntries;
+    };
+    uint4* const dc = deep + (size_t)(kDeepChains * c + ch) * kDeepLevels;
+    for (uint32_t k = 0; k < kDeepLevels; ++k) {
+      uint4 dr = make_uint4(0, 0, 0, 0);
+      if (x != ~0ull && deep_at(x)) {
+        const uint64_t db = ip0 + ((x - ip0) / kC) * kC;
+        uint64_t dex, dot;
+        dev_walk<kC>(in, N, x, min(db + kC, (uint64_t)N - 1), wjt, lane, stg, dex, dot);
+        dr = make_uint4((uint32_t)x, (uint32_t)min(dex, (uint64_t)0xffffffffu),
+                        (uint32_t)min(dot, (uint64_t)0xffffffffu), 1u);
+        x = dex;
+      }
+      if (lane == 0) dc[k] = dr;
+      if (!dr.w) {
+        for (uint32_t j = k + 1; j < kDeepLevels; ++j)
+          if (lane == 0) dc[j] = make_uint4(0, 0, 0, 0);
+        break;
       }
     }
   }
@@ -1320,7 +1341,6 @@ __global__ __launch_bounds__(64) void k_origin_fill(const uint8_t* __restrict__ 
 // launches and gathered -- one synchronisation for the whole call.  Any stream (no block
 // structure assumed); anything unexpected (an error, no progress, a length mismatch) is reported
 // in ctl[1] and the caller decodes the old way, which also finds the first error.
-constexpr uint32_t kFillStage = kSmallChunk + kIdxPad + 256;  // an element's tags and a window past them
 // The chain's LDS pool (u32 words): the entry records of the first chunks, compact (below), then
 // the deep records of as many chunks as still fit.  Everything else is read from HBM.
 constexpr uint32_t kChainThreads = 1024;  // all of them load the pool and take part in the runs
@@ -1351,6 +1371,7 @@ __device__ inline uint32_t rec_compact(uint2 r, uint64_t base) {
 // Every run element is one the serial chain would take (same record, same exit), so the path is
 // identical; anything else (deep entries, walks, records not in LDS) stays serial.
 // ctl[0] = path elements, ctl[1] = 0 (the path covers exactly `size` bytes of output) or 1 (fall back)
+template <uint32_t kC>  // bytes per index chunk
 __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
                                                                 uint32_t size, uint32_t nchunks,
                                                                 const uint2* __restrict__ rec,
@@ -1362,7 +1383,7 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
   __shared__ uint32_t Dsh[kChainNodes], SSsh[kChainNodes], Esh[kChainNodes], Wsh[kChainNodes];
   __shared__ uint32_t run[5];  // the run wave 0 asks for: c1 (kRunDone: finished), y, O, np, output of c1's element
   __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
-  __shared__ __attribute__((aligned(16))) uint8_t stg[kDevWalkStage + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t stg[kC + kIdxPad + 16];
   // one round trip for the whole pool: every thread's loads are in flight before its stores
   const uint32_t nrec = min(nchunks, kChainPool / kIdxEntries);                    // chunks with LDS records
   const uint32_t ndeep = min(nchunks, (kChainPool - nrec * kIdxEntries) / kDeepWords);  // ... and LDS deep records
@@ -1378,7 +1399,7 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const uint32_t k = k0 + u * kChainThreads;
-        if (k < nr) srec[k] = rec_compact(v[u], ip0 + (uint64_t)(k / kIdxEntries) * kSmallChunk);
+        if (k < nr) srec[k] = rec_compact(v[u], ip0 + (uint64_t)(k / kIdxEntries) * kC);
       }
     }
     for (uint32_t k0 = t; k0 < nd; k0 += 4 * kChainThreads) {
@@ -1390,16 +1411,21 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
     }
   }
   __syncthreads();
-  const bool par = nchunks <= kChainNodes && nrec == nchunks;
+  const bool par = nchunks <= kChainNodes;
+  // a compact entry record from LDS, or from HBM past the pool
+  auto crec = [&](uint32_t cc, uint32_t l) {
+    return cc < nrec ? srec[cc * kIdxEntries + l]
+                     : rec_compact(rec[cc * kIdxEntries + l], ip0 + (uint64_t)cc * kC);
+  };
   if (par) {  // the links and their pointer jumping (a root links to itself)
     uint32_t link = t, w = 0, e = 0xffffffffu;
     if (t < nchunks) {
-      const uint32_t v0 = srec[t * kIdxEntries];
+      const uint32_t v0 = crec(t, 0);
       if (v0 != kRecNone) {
-        e = ip0 + t * kSmallChunk + (v0 & 0xffffu);
-        const uint32_t er = e - ip0, c2 = er / kSmallChunk, l2 = er % kSmallChunk;
+        e = ip0 + t * kC + (v0 & 0xffffu);
+        const uint32_t er = e - ip0, c2 = er / kC, l2 = er % kC;
         if ((uint64_t)e < (uint64_t)N - 1 && l2 < kIdxEntries && c2 < nchunks && c2 > t) {
-          const uint32_t v2 = srec[c2 * kIdxEntries + l2], v20 = srec[c2 * kIdxEntries];
+          const uint32_t v2 = crec(c2, l2), v20 = crec(c2, 0);
           if (v2 != kRecNone && v20 != kRecNone && (v2 & 0xffffu) == (v20 & 0xffffu) && (v2 & 0xffffu) > l2) {
             link = c2;
             w = v2 >> 16;
@@ -1452,11 +1478,11 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
           uint32_t yr = (uint32_t)(y - ip0);
           bool stop = false;
           while (true) {
-            const uint32_t c = yr / kSmallChunk, l = yr % kSmallChunk;
-            if (l >= kIdxEntries || c >= nrec) break;
-            const uint32_t v = uniform(srec[c * kIdxEntries + l]), d = v & 0xffffu;
+            const uint32_t c = yr / kC, l = yr % kC;
+            if (l >= kIdxEntries || c >= nchunks) break;
+            const uint32_t v = uniform(crec(c, l)), d = v & 0xffffu;
             if (v == kRecNone || d <= l || np >= nchunks) break;
-            const uint32_t ot = v >> 16, exr = c * kSmallChunk + d, Oc = (uint32_t)O;  // (O <= size here)
+            const uint32_t ot = v >> 16, exr = c * kC + d, Oc = (uint32_t)O;  // (O <= size here)
             if (par && uniform(Dsh[c]) >= kMinRun && ip0 + exr == uniform(Esh[c])) {  // a run from here
               c1 = c;
               out1 = ot;
@@ -1477,8 +1503,8 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
           y = ip0 + (uint64_t)yr;
           if (stop || c1 != kRunDone) break;
         }
-        const uint32_t c = (uint32_t)((y - ip0) / kSmallChunk);
-        const uint64_t base = ip0 + (uint64_t)c * kSmallChunk, l = y - base;
+        const uint32_t c = (uint32_t)((y - ip0) / kC);
+        const uint64_t base = ip0 + (uint64_t)c * kC, l = y - base;
         uint64_t ex, ot;
         if (l < kIdxEntries) {
           const uint32_t v = c < nrec ? srec[c * kIdxEntries + l] : kRecNone;
@@ -1510,7 +1536,7 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
             dsrc = i / kDeepLevels;
             dlev = i % kDeepLevels;
           } else {
-            dev_walk(in, N, y, min(base + kSmallChunk, (uint64_t)N - 1), jt, lane, stg, ex, ot);
+            dev_walk<kC>(in, N, y, min(base + kC, (uint64_t)N - 1), jt, lane, stg, ex, ot);
             dsrc = 0xffffffffu;
           }
         }
@@ -1578,18 +1604,19 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
 }
 
 // k_origin_fill for the device chain's path: elements past ctl[0] exit; a failing element sets ctl[2]
+template <uint32_t kC>  // bytes per index chunk
 __global__ __launch_bounds__(64) void k_origin_fill_dev(const uint8_t* __restrict__ in, uint32_t N, uint32_t size,
                                                         const OriginPath* path, uint32_t* __restrict__ P,
                                                         uint32_t* ctl) {
   __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
-  __shared__ __attribute__((aligned(16))) uint8_t buf[kFillStage + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t buf[kC + kIdxPad + 256 + 16];  // an element's tags and a window past them
   const uint32_t npath = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t fail = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // (both in flight)
   if (blockIdx.x >= uniform(npath) || uniform(fail)) return;
   const OriginPath pe = path[blockIdx.x];
-  stage_bytes(buf, in, N, pe.y, kFillStage, lane_id());  // (zero past N, as load8z)
+  stage_bytes(buf, in, N, pe.y, kC + kIdxPad + 256, lane_id());  // (zero past N, as load8z)
   __syncthreads();
-  const int32_t st = origin_walk<true>(in, N, size, pe, P, jt, lane_id(), buf, pe.y, kFillStage);
+  const int32_t st = origin_walk<true>(in, N, size, pe, P, jt, lane_id(), buf, pe.y, kC + kIdxPad + 256);
   if (st != kOk && lane_id() == 0) atomicOr(&ctl[2], 1u);
 }
 
@@ -1708,16 +1735,27 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
   return hipGetLastError();
 }
 
-hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
-                               uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
-                               uint8_t* out, uint32_t* words, hipStream_t s) {
-  if (nchunks == 0 || size == 0 || rounds == 0 || 4 + rounds > kWave) return hipErrorInvalidValue;
+template <uint32_t kC>
+static void launch_small_front(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks, uint32_t* rec,
+                               OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds, hipStream_t s) {
   uint4* deep = reinterpret_cast<uint4*>(rec + (size_t)nchunks * kIdxEntries * 2);  // kDeepChains x kDeepLevels per chunk
-  hipLaunchKernelGGL((k_stream_index<kSmallChunk, true>), dim3(nchunks), dim3(64), 0, s, in, N, ip0,
+  hipLaunchKernelGGL((k_stream_index<kC, true>), dim3(nchunks), dim3(index_threads(true)), 0, s, in, N, ip0,
                      reinterpret_cast<uint2*>(rec), deep);
-  hipLaunchKernelGGL(k_stream_chain, dim3(1), dim3(kChainThreads), 0, s, in, N, ip0, size, nchunks,
+  hipLaunchKernelGGL(k_stream_chain<kC>, dim3(1), dim3(kChainThreads), 0, s, in, N, ip0, size, nchunks,
                      reinterpret_cast<const uint2*>(rec), deep, path, ctl, rounds);
-  hipLaunchKernelGGL(k_origin_fill_dev, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
+  hipLaunchKernelGGL(k_origin_fill_dev<kC>, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
+}
+
+hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t chunk,
+                               uint32_t nchunks, uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P,
+                               uint32_t rounds, uint8_t* out, uint32_t* words, hipStream_t s) {
+  if (nchunks == 0 || size == 0 || rounds == 0 || 4 + rounds > kWave) return hipErrorInvalidValue;
+  if (chunk == kSmallChunk)
+    launch_small_front<kSmallChunk>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
+  else if (chunk == kSmallChunkFine)
+    launch_small_front<kSmallChunkFine>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
+  else
+    return hipErrorInvalidValue;
   // later launches usually find nothing pending and return at once: a small grid dispatches
   // faster, and strides over the pointers when some are left
   const uint32_t g1 = min(32768u, max(1u, (size + 255) / 256));

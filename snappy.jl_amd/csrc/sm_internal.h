@@ -53,10 +53,11 @@ hipError_t launch_decompress(const DecompressArgs& a, int large, hipStream_t s);
 // compressed body, then one wave per 64 KiB output fragment (see sm_decompress.hip).
 constexpr uint32_t kIdxChunk = 4096;  // compressed bytes per index chunk
 constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
-#ifndef SM_SMALL_CHUNK
-#define SM_SMALL_CHUNK 1024
-#endif
-constexpr uint32_t kSmallChunk = SM_SMALL_CHUNK;  // path 4 (a small stream on the device): bytes per index chunk
+// path 4 (a small stream on the device): bytes per index chunk -- kSmallChunkFine for bodies of
+// mostly copies (shorter index and fill latency per chunk), kSmallChunk when literals are long or
+// the body large (fewer chain elements).  sm_api.hip small_chunk() picks.
+constexpr uint32_t kSmallChunk = 1024;
+constexpr uint32_t kSmallChunkFine = 512;
 #ifndef SM_SMALL_HOPS
 #define SM_SMALL_HOPS 1024
 #endif
@@ -101,9 +102,9 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
 // bytes in the launch that resolves it) and words[0..1] = ctl[1], ctl[2]; the last launch sets
 // words[2] = 1 when a pointer is still unresolved after it (the caller zeroes words[2] first).  Any
 // nonzero word: fall back.  out and words may be device-mapped pinned host memory.
-hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks,
-                               uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds,
-                               uint8_t* out, uint32_t* words, hipStream_t s);
+hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t chunk,
+                               uint32_t nchunks, uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P,
+                               uint32_t rounds, uint8_t* out, uint32_t* words, hipStream_t s);
 // src[0, n) to dst and wsrc[0, nw) to words by a kernel (dst, words: device-mapped pinned host
 // memory; no copy engine behind the kernels).  src, dst 16-byte aligned; nw <= 256.
 hipError_t launch_to_host(const uint8_t* src, uint32_t n, uint8_t* dst, const uint32_t* wsrc, uint32_t nw,
