@@ -28,9 +28,15 @@ constexpr uint32_t kScreenTodo = 0xfffffffeu;  // out_len mark of k_literal_scre
 // and a block with fewer than kScrMin repeated anchors has ~kScrMin x 64 B of repeats at most.
 constexpr uint32_t kScrMin = 8;           // repeated anchors that make a block "compressible"
 constexpr uint32_t kScrMinLen = 8192;     // smaller blocks always take the parse
-constexpr uint32_t kScrThreads = 512;
+#ifndef SM_SCR_THREADS
+#define SM_SCR_THREADS 512
+#endif
+#ifndef SM_SCR_FIRST
+#define SM_SCR_FIRST 1
+#endif
+constexpr uint32_t kScrThreads = SM_SCR_THREADS;
 constexpr uint32_t kScrPieces = kBlockSize / 16 / kScrThreads;  // 16-B pieces per thread (8)
-constexpr uint32_t kScrFirst = 1;                               // pieces of the first pass (8 KiB)
+constexpr uint32_t kScrFirst = SM_SCR_FIRST;                    // pieces of the first pass (8 KiB)
 constexpr uint32_t kScrTabBits = 12;
 constexpr uint32_t kScrEmpty = 0xffffffffu;  // its hash is no anchor, so no anchor word equals it
 static_assert(((kScrEmpty * kHashMul) >> 26) != 0, "the empty mark must not be an anchor word");

@@ -806,6 +806,67 @@ def test_uncompress_small_streams_device_path(sm, oracle, libsnappy, gpu_availab
                 assert out_g == out_o
 
 
+def _fine_chunks(sm, s):
+    """sm_api.hip small_chunk(): 512-byte index chunks for bodies <= 0.6 of the output and 256 KiB."""
+    size, hdr = sm.parse32(s)
+    body = len(s) - hdr
+    return body * 10 <= size * 6 and body <= 256 << 10
+
+
+def test_small_path_chunk_sizes_and_parallel_runs(sm, oracle, gpu_available):
+    """Path 4's two index chunk sizes (sm_api.hip small_chunk) and the chain's parallel runs
+    (sm_decompress.hip k_stream_chain: pointer-jumped chunk links, serial steps between): bodies
+    of exactly 1, 2 and many 512-byte chunks, both sides of the size rule's bounds, long copy runs
+    (runs of >= kMinRun links) broken by long literals (deep entries, then a new run), and
+    mutations of such streams.  Output and status equal the oracle's."""
+    from streams import build
+    rng = np.random.default_rng(512)
+    cases = []
+
+    def copy_run(body, lit=60):  # copy-2 tags after one literal: a body of exactly `body` bytes
+        ops, left = [("lit", rng.integers(0, 256, lit, dtype=np.uint8).tobytes())], body - lit - 1
+        while left > 61:
+            ops.append(("copy", 60, 60))
+            left -= 3
+        ops.append(("lit", rng.integers(0, 256, left - 1, dtype=np.uint8).tobytes()))
+        return build(ops)
+
+    for body in (512, 513, 1024, 1025, 4096 + 512, 256 << 10, (256 << 10) + 1):
+        cases.append(copy_run(body))
+    # runs broken by literal groups: ratio below and above the fine-chunk rule
+    for lit_hi, groups, cp_lo, cp_hi in ((700, 60, 200, 900), (1500, 40, 200, 900), (4000, 30, 10, 60)):
+        ops, size = [("lit", rng.integers(0, 256, 64, dtype=np.uint8).tobytes())], 64
+        for _ in range(groups):
+            for _ in range(int(rng.integers(1, 4))):
+                ops.append(("lit", rng.integers(0, 256, int(rng.integers(65, lit_hi)), dtype=np.uint8).tobytes()))
+                size += len(ops[-1][1])
+            for _ in range(int(rng.integers(cp_lo, cp_hi))):
+                ops.append(("copy", int(rng.integers(1, min(3000, size) + 1)), int(rng.integers(4, 65))))
+                size += ops[-1][2]
+        cases.append(build(ops))
+    fine = [_fine_chunks(sm, s) for s, _ in cases]
+    assert any(fine) and not all(fine)
+    for s, e in cases:
+        assert oracle.uncompress(s) == e
+        assert sm.uncompress(s) == e, len(e)
+        if small_path(sm, s):
+            assert sm.last_uncompress_path() == 4
+    assert sum(small_path(sm, s) for s, _ in cases) >= len(cases) - 2
+    for s, _ in cases[-3:]:
+        for _ in range(10):
+            bad = bytearray(s)
+            bad[int(rng.integers(2, len(bad)))] = int(rng.integers(0, 256))
+            bad = bytes(bad)
+            st_o, out_o = oracle.uncompress_status(bad)
+            try:
+                st_g, out_g = 0, sm.uncompress(bad)
+            except sm.SnappyError as exc:
+                st_g, out_g = exc.code, None
+            assert st_g == st_o
+            if st_o == 0:
+                assert out_g == out_o
+
+
 def test_host_path_piece_boundaries(sm, oracle, gpu_available):
     """The single-buffer host path's pipelining (sm_api.hip): inputs from 32 MiB upload in
     16 MiB pieces with per-piece compress kernels, outputs over 128 MiB download in pieces under
