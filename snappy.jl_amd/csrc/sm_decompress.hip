@@ -886,139 +886,139 @@ __global__ __launch_bounds__(index_threads(kDeep)) void k_stream_index(const uin
   const uint32_t c = blockIdx.x, lane = lane_id(), wv = threadIdx.x / kWave;
   const uint32_t s = ip0 + c * kC;
   if (wv == 0) {  // (one wave from here to the chain starts: LDS in order, signal fences only)
-  stage_bytes(buf, in, N, s, kC + kIdxPad, lane);
-  for (uint32_t k = lane; k < kC / 32; k += kWave) bm[k] = 0;
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  const uint64_t lim = min((uint64_t)s + kC, (uint64_t)N - 1);  // tags start below N-1 (:416)
-  // lane 0's path: the tag walk from the chunk's first byte, a 256-byte window at a time
-  uint64_t p = s, acc = 0, size, outb;
-  while (p < lim) {
-    const uint32_t rel0 = (uint32_t)(p - s);
-    uint32_t rel, next, ob, excl;
-    const uint32_t ntok = window_tags(buf, rel0, (uint32_t)min(lim - p, (uint64_t)256), jt, lane, rel, next, ob, excl);
-    if (ntok == 0) {  // long literal
-      if (lane == 0) {
-        bm[rel0 >> 5] |= 1u << (rel0 & 31);
-        cum[rel0] = (uint32_t)acc;
+    stage_bytes(buf, in, N, s, kC + kIdxPad, lane);
+    for (uint32_t k = lane; k < kC / 32; k += kWave) bm[k] = 0;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint64_t lim = min((uint64_t)s + kC, (uint64_t)N - 1);  // tags start below N-1 (:416)
+    // lane 0's path: the tag walk from the chunk's first byte, a 256-byte window at a time
+    uint64_t p = s, acc = 0, size, outb;
+    while (p < lim) {
+      const uint32_t rel0 = (uint32_t)(p - s);
+      uint32_t rel, next, ob, excl;
+      const uint32_t ntok = window_tags(buf, rel0, (uint32_t)min(lim - p, (uint64_t)256), jt, lane, rel, next, ob, excl);
+      if (ntok == 0) {  // long literal
+        if (lane == 0) {
+          bm[rel0 >> 5] |= 1u << (rel0 & 31);
+          cum[rel0] = (uint32_t)acc;
+        }
+        tag_at(buf, rel0, size, outb);
+        acc += outb;
+        p += size;
+        continue;
       }
-      tag_at(buf, rel0, size, outb);
-      acc += outb;
-      p += size;
-      continue;
+      if (lane < ntok) {
+        atomicOr(&bm[rel >> 5], 1u << (rel & 31));
+        cum[rel] = (uint32_t)acc + excl;
+      }
+      acc += readlane(excl + ob, ntok - 1);
+      p = s + readlane(next, ntok - 1);
     }
-    if (lane < ntok) {
-      atomicOr(&bm[rel >> 5], 1u << (rel & 31));
-      cum[rel] = (uint32_t)acc + excl;
-    }
-    acc += readlane(excl + ob, ntok - 1);
-    p = s + readlane(next, ntok - 1);
-  }
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  const uint64_t exit0 = p;
-  const uint32_t tot0 = (uint32_t)acc;
-  // Lanes 1..63 (entries at chunk bytes 1..63) walk until they meet lane 0's path or leave the
-  // chunk, a 256-byte window at a time, by pointer doubling with lane 0's path as stop nodes:
-  // J0[x] = x + size(x), O0[x] = its output bytes; a path position, a long literal or a
-  // position at/after the limit is a fixed point (O = 0).  Seven doublings give 128 steps --
-  // more tags than 256 bytes hold -- so J7[x] is where the walk from x meets the path, stops or
-  // leaves the window, and O7[x] the output on the way.  Long literals take a scalar step.
-  const uint64_t rl = lim > s ? lim - s : 0;  // chunk-relative parse limit
-  uint64_t x = lane, ex = exit0;
-  uint32_t pre = 0, res = tot0;
-  bool done = lane == 0 || SM_IDX_NOLANES;  // (SM_IDX_NOLANES: timing variant only)
-  uint16_t* tj = jt;                                   // 2 x 256 u16
-  uint32_t* to = reinterpret_cast<uint32_t*>(jt + 512);  // 2 x 256 u32 (jt holds 3 KiB here)
-  while (true) {
-    bool again = true;
-    while (ballot(again)) {  // settle: out of the chunk, on the path, or a long literal
-      again = false;
-      if (!done) {
-        if (x >= rl) {
-          ex = s + x;
-          res = pre;
-          done = true;
-        } else if ((bm[x >> 5] >> (x & 31)) & 1u) {  // met lane 0's path
-          res = pre + (tot0 - cum[x]);
-          done = true;
-        } else {
-          tag_at(buf, (uint32_t)x, size, outb);
-          if (walk_stop_literal(buf[x], outb)) {
-            pre += (uint32_t)outb;
-            x += size;
-            again = true;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const uint64_t exit0 = p;
+    const uint32_t tot0 = (uint32_t)acc;
+    // Lanes 1..63 (entries at chunk bytes 1..63) walk until they meet lane 0's path or leave the
+    // chunk, a 256-byte window at a time, by pointer doubling with lane 0's path as stop nodes:
+    // J0[x] = x + size(x), O0[x] = its output bytes; a path position, a long literal or a
+    // position at/after the limit is a fixed point (O = 0).  Seven doublings give 128 steps --
+    // more tags than 256 bytes hold -- so J7[x] is where the walk from x meets the path, stops or
+    // leaves the window, and O7[x] the output on the way.  Long literals take a scalar step.
+    const uint64_t rl = lim > s ? lim - s : 0;  // chunk-relative parse limit
+    uint64_t x = lane, ex = exit0;
+    uint32_t pre = 0, res = tot0;
+    bool done = lane == 0 || SM_IDX_NOLANES;  // (SM_IDX_NOLANES: timing variant only)
+    uint16_t* tj = jt;                                   // 2 x 256 u16
+    uint32_t* to = reinterpret_cast<uint32_t*>(jt + 512);  // 2 x 256 u32 (jt holds 3 KiB here)
+    while (true) {
+      bool again = true;
+      while (ballot(again)) {  // settle: out of the chunk, on the path, or a long literal
+        again = false;
+        if (!done) {
+          if (x >= rl) {
+            ex = s + x;
+            res = pre;
+            done = true;
+          } else if ((bm[x >> 5] >> (x & 31)) & 1u) {  // met lane 0's path
+            res = pre + (tot0 - cum[x]);
+            done = true;
+          } else {
+            tag_at(buf, (uint32_t)x, size, outb);
+            if (walk_stop_literal(buf[x], outb)) {
+              pre += (uint32_t)outb;
+              x += size;
+              again = true;
+            }
           }
         }
       }
-    }
-    if (!ballot(!done)) break;
-    uint32_t base = done ? 0xffffffffu : (uint32_t)x;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) base = min(base, (uint32_t)__shfl_xor(base, d, 64));
-    const uint32_t rlim = (uint32_t)min(rl - base, (uint64_t)256);
-    const uint64_t cw = lds_ld64(buf, base + 4 * lane);
-    const uint32_t sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
-    uint32_t J[4], O[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t r = 4 * lane + j, a = base + r, sz = (sizes >> (8 * j)) & 0xff, cb = (uint32_t)(cw >> (8 * j)) & 0xff;
-      const uint32_t e = char_entry(cb);
-      const bool stop = r >= rlim || ((bm[a >> 5] >> (a & 31)) & 1u) || sz == 255;  // (bm read below rlim only)
-      J[j] = stop ? r : r + sz;
-      O[j] = stop ? 0u : (cb & 3) ? (e & 0xff) : sz - 1 - (e >> 11);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {  // k = 7: the final tables for the lanes' read
-      uint16_t* bj = tj + (k & 1) * 256;
-      uint32_t* bo = to + (k & 1) * 256;
-#pragma unroll
+      if (!ballot(!done)) break;
+      uint32_t base = done ? 0xffffffffu : (uint32_t)x;
+  #pragma unroll
+      for (int d = 1; d < 64; d <<= 1) base = min(base, (uint32_t)__shfl_xor(base, d, 64));
+      const uint32_t rlim = (uint32_t)min(rl - base, (uint64_t)256);
+      const uint64_t cw = lds_ld64(buf, base + 4 * lane);
+      const uint32_t sizes = pack_sizes((uint32_t)cw, (uint32_t)(cw >> 32));
+      uint32_t J[4], O[4];
+  #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        bj[4 * lane + j] = (uint16_t)J[j];
-        bo[4 * lane + j] = O[j];
+        const uint32_t r = 4 * lane + j, a = base + r, sz = (sizes >> (8 * j)) & 0xff, cb = (uint32_t)(cw >> (8 * j)) & 0xff;
+        const uint32_t e = char_entry(cb);
+        const bool stop = r >= rlim || ((bm[a >> 5] >> (a & 31)) & 1u) || sz == 255;  // (bm read below rlim only)
+        J[j] = stop ? r : r + sz;
+        O[j] = stop ? 0u : (cb & 3) ? (e & 0xff) : sz - 1 - (e >> 11);
       }
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      if (k == 7) break;
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (J[j] < 256) {
-          O[j] += bo[J[j]];
-          J[j] = bj[J[j]];
+  #pragma unroll
+      for (int k = 0; k < 8; ++k) {  // k = 7: the final tables for the lanes' read
+        uint16_t* bj = tj + (k & 1) * 256;
+        uint32_t* bo = to + (k & 1) * 256;
+  #pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          bj[4 * lane + j] = (uint16_t)J[j];
+          bo[4 * lane + j] = O[j];
         }
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    }
-    if (!done && x < base + 256) {
-      const uint32_t r = (uint32_t)x - base;
-      pre += to[256 + r];
-      x = base + tj[256 + r];
-    }
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the next window's stores follow these reads
-  }
-  // (exit, output) pairs side by side: the host's walk over the records reads one cache line
-  rec[c * kIdxEntries + lane] = make_uint2((uint32_t)min(ex, (uint64_t)0xffffffffu), res);
-  if constexpr (kDeep) {
-    // chain 0 starts at lane 0's exit; chains 1.. at other distinct exits of the entry lanes that
-    // land kIdxEntries or more bytes into a chunk (the records there do not cover them: a walk
-    // that did not meet lane 0's path, e.g. one inside a long literal).  tools/chain_model.py
-    // --distinct: paper-100k.pdf's fast stream 19 chain walks with one chain, 7 with four.
-    auto deep_at = [&](uint64_t v) {
-      const uint64_t db = ip0 + ((v - ip0) / kC) * kC;
-      return v < (uint64_t)N - 1 && v - db >= kIdxEntries;
-    };
-    // (only exits inside the next chunk: the entry lanes that are not on the stream's path read
-    // garbage as tags and often jump far -- chains for those cost alice29.txt 10 us, and the
-    // model finds the same 7 walks on paper-100k.pdf without them)
-    const uint32_t ex32 = (uint32_t)min(ex, (uint64_t)0xffffffffu);
-    uint64_t more = ballot(ex != exit0 && ex < (uint64_t)s + 2 * kC && deep_at(ex));
-    for (uint32_t ch = 0; ch < kDeepChains; ++ch) {
-      uint64_t x = ~0ull;  // (no chain: zero records)
-      if (ch == 0) {
-        x = exit0;
-      } else if (more) {
-        x = readlane(ex32, ctz64(more));
-        more &= ballot(ex32 != (uint32_t)x);
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (k == 7) break;
+  #pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (J[j] < 256) {
+            O[j] += bo[J[j]];
+            J[j] = bj[J[j]];
+          }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
       }
-      if (lane == 0) xs[ch] = x;
+      if (!done && x < base + 256) {
+        const uint32_t r = (uint32_t)x - base;
+        pre += to[256 + r];
+        x = base + tj[256 + r];
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the next window's stores follow these reads
     }
-  }
+    // (exit, output) pairs side by side: the host's walk over the records reads one cache line
+    rec[c * kIdxEntries + lane] = make_uint2((uint32_t)min(ex, (uint64_t)0xffffffffu), res);
+    if constexpr (kDeep) {
+      // chain 0 starts at lane 0's exit; chains 1.. at other distinct exits of the entry lanes that
+      // land kIdxEntries or more bytes into a chunk (the records there do not cover them: a walk
+      // that did not meet lane 0's path, e.g. one inside a long literal).  tools/chain_model.py
+      // --distinct: paper-100k.pdf's fast stream 19 chain walks with one chain, 7 with four.
+      auto deep_at = [&](uint64_t v) {
+        const uint64_t db = ip0 + ((v - ip0) / kC) * kC;
+        return v < (uint64_t)N - 1 && v - db >= kIdxEntries;
+      };
+      // (only exits inside the next chunk: the entry lanes that are not on the stream's path read
+      // garbage as tags and often jump far -- chains for those cost alice29.txt 10 us, and the
+      // model finds the same 7 walks on paper-100k.pdf without them)
+      const uint32_t ex32 = (uint32_t)min(ex, (uint64_t)0xffffffffu);
+      uint64_t more = ballot(ex != exit0 && ex < (uint64_t)s + 2 * kC && deep_at(ex));
+      for (uint32_t ch = 0; ch < kDeepChains; ++ch) {
+        uint64_t x = ~0ull;  // (no chain: zero records)
+        if (ch == 0) {
+          x = exit0;
+        } else if (more) {
+          x = readlane(ex32, ctz64(more));
+          more &= ballot(ex32 != (uint32_t)x);
+        }
+        if (lane == 0) xs[ch] = x;
+      }
+    }
   }  // (wave 0)
   if constexpr (kDeep) {
     __syncthreads();
