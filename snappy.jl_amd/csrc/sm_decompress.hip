@@ -1352,6 +1352,9 @@ constexpr uint32_t kChainNodes = kChainThreads;  // chunks the parallel runs cov
 constexpr uint32_t kLift = 10;                   // 2^kLift >= kChainNodes: jump tables J[0..kLift)
 constexpr uint32_t kMinRun = 8;                  // links ahead that make a parallel run worth two barriers
 constexpr uint32_t kRunDone = 0xffffffffu;
+#ifndef SM_CHAIN_DEEPLINK
+#define SM_CHAIN_DEEPLINK 1  // links through chain 0's deep records (0: entry records only)
+#endif
 static_assert((1u << kLift) >= kChainNodes, "the jump tables must reach every node");
 // an entry record (exit, output) of chunk base `base`, compact: (output << 16) | (exit - base)
 __device__ inline uint32_t rec_compact(uint2 r, uint64_t base) {
@@ -1370,6 +1373,17 @@ __device__ inline uint32_t rec_compact(uint2 r, uint64_t base) {
 // node i - 1 along is t) and writes its own path element; wave 0 continues after the last.
 // Every run element is one the serial chain would take (same record, same exit), so the path is
 // identical; anything else (deep entries, walks, records not in LDS) stays serial.
+__device__ inline uint4 chain_deep0(const uint4* sdeep, const uint4* __restrict__ deep, uint32_t nsdeep, uint32_t c,
+                                    uint32_t k) {
+  const uint32_t i = kDeepLevels * kDeepChains * c + k;
+  uint4 v;
+  if (i < nsdeep)
+    v = sdeep[i];
+  else
+    v = deep[i];
+  return v;
+}
+
 // ctl[0] = path elements, ctl[1] = 0 (the path covers exactly `size` bytes of output) or 1 (fall back)
 template <uint32_t kC>  // bytes per index chunk
 __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip0,
@@ -1380,7 +1394,11 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
   __shared__ __attribute__((aligned(16))) uint32_t pool[kChainPool];
   __shared__ __attribute__((aligned(16))) OriginPath spath[kChainPath];
   __shared__ uint16_t J[kLift][kChainNodes];
-  __shared__ uint32_t Dsh[kChainNodes], SSsh[kChainNodes], Esh[kChainNodes], Wsh[kChainNodes];
+  // per chunk node: D (links to the end, low 16 bits) | elements before the end's (high 16), the
+  // output on the way (saturating), E, the output of the linked element, of the deep elements
+  // before it, and their count
+  __shared__ uint32_t Dsh[kChainNodes], SSsh[kChainNodes], Esh[kChainNodes], Wsh[kChainNodes], Wdsh[kChainNodes];
+  __shared__ uint8_t Lsh[kChainNodes];
   __shared__ uint32_t run[5];  // the run wave 0 asks for: c1 (kRunDone: finished), y, O, np, output of c1's element
   __shared__ __attribute__((aligned(16))) uint16_t jt[kJt];
   __shared__ __attribute__((aligned(16))) uint8_t stg[kC + kIdxPad + 16];
@@ -1417,34 +1435,57 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
     return cc < nrec ? srec[cc * kIdxEntries + l]
                      : rec_compact(rec[cc * kIdxEntries + l], ip0 + (uint64_t)cc * kC);
   };
+  // chain 0's deep record k of chunk c (LDS, or HBM past the pool)
+  const uint32_t nsdeep = ndeep * kDeepChains * kDeepLevels;
+#define drec0(c, k) chain_deep0(sdeep, deep, nsdeep, (c), (k))
   if (par) {  // the links and their pointer jumping (a root links to itself)
-    uint32_t link = t, w = 0, e = 0xffffffffu;
+    uint32_t link = t, w = 0, wd = 0, nd = 0, e = 0xffffffffu;
     if (t < nchunks) {
       const uint32_t v0 = crec(t, 0);
       if (v0 != kRecNone) {
         e = ip0 + t * kC + (v0 & 0xffffu);
-        const uint32_t er = e - ip0, c2 = er / kC, l2 = er % kC;
-        if ((uint64_t)e < (uint64_t)N - 1 && l2 < kIdxEntries && c2 < nchunks && c2 > t) {
-          const uint32_t v2 = crec(c2, l2), v20 = crec(c2, 0);
-          if (v2 != kRecNone && v20 != kRecNone && (v2 & 0xffffu) == (v20 & 0xffffu) && (v2 & 0xffffu) > l2) {
-            link = c2;
-            w = v2 >> 16;
+        // from E(t): through chain 0's deep records while the exits land deep in later chunks
+        // (the serial chain takes exactly those: level 0 from the chains of t's chunk, level k + 1
+        // as the next level of the record it came from), then a recorded entry that exits at E
+        uint32_t X = e;
+        for (uint32_t k = 0; k <= kDeepLevels; ++k) {
+          const uint32_t xr = X - ip0, cx = xr / kC, lx = xr % kC;
+          if ((uint64_t)X >= (uint64_t)N - 1 || cx >= nchunks || cx <= t) break;
+          if (lx < kIdxEntries) {
+            const uint32_t v2 = crec(cx, lx), v20 = crec(cx, 0);
+            if (v2 != kRecNone && v20 != kRecNone && (v2 & 0xffffu) == (v20 & 0xffffu) && (v2 & 0xffffu) > lx) {
+              link = cx;
+              w = v2 >> 16;
+            }
+            break;
           }
+          if (!SM_CHAIN_DEEPLINK || k == kDeepLevels) break;
+          const uint4 dr = drec0(t, k);
+          if (!(dr.w && dr.x == X && dr.y > X && dr.z <= size)) break;
+          ++nd;
+          wd += dr.z;  // (<= kDeepLevels * size: no wrap for size < 2^30)
+          X = dr.y;
+        }
+        if (link == t || wd > size) {
+          link = t;
+          w = wd = nd = 0;
         }
       }
     }
     Esh[t] = e;
     Wsh[t] = w;
+    Wdsh[t] = wd;
+    Lsh[t] = (uint8_t)nd;
     J[0][t] = (uint16_t)link;
-    uint32_t d = link != t ? 1u : 0u, ss = w, p = link;
+    uint32_t d = link != t ? 1u | ((1u + nd) << 16) : 0u, ss = w + wd, p = link;
     Dsh[t] = d;
     SSsh[t] = ss;
     __syncthreads();
     for (uint32_t r = 1; r <= kLift; ++r) {  // d, ss: over 2^r links; J[r] = J[r-1] o J[r-1]
       const uint32_t dp = Dsh[p], sp = SSsh[p], pn = J[r - 1][p];
       __syncthreads();
-      d += dp;
-      ss += sp;
+      d += dp;  // (both halves: at most kChainNodes each)
+      ss = ss + sp < ss ? 0xffffffffu : ss + sp;  // (saturating: a run then ends past `size`, rejected)
       Dsh[t] = d;
       SSsh[t] = ss;
       if (r < kLift) J[r][t] = (uint16_t)pn;
@@ -1483,7 +1524,7 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
             const uint32_t v = uniform(crec(c, l)), d = v & 0xffffu;
             if (v == kRecNone || d <= l || np >= nchunks) break;
             const uint32_t ot = v >> 16, exr = c * kC + d, Oc = (uint32_t)O;  // (O <= size here)
-            if (par && uniform(Dsh[c]) >= kMinRun && ip0 + exr == uniform(Esh[c])) {  // a run from here
+            if (par && (uniform(Dsh[c]) & 0xffffu) >= kMinRun && ip0 + exr == uniform(Esh[c])) {  // a run from here
               c1 = c;
               out1 = ot;
               break;
@@ -1567,20 +1608,42 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
     __syncthreads();
     const uint32_t c1 = run[0];
     if (c1 == kRunDone) break;
-    {  // every chunk: is it i links along from c1?  Then its element is path element np + i.
-      const uint32_t y1 = run[1], O1 = run[2], np1 = run[3], out1 = run[4], D1 = Dsh[c1];
-      if (t < nchunks && t >= c1 && Dsh[t] <= D1) {
-        const uint32_t i = D1 - Dsh[t];
+    {  // every chunk: is it i links along from c1?  Then its element is path element np + (the
+       // elements between), followed by its link's deep elements.
+      const uint32_t y1 = run[1], O1 = run[2], np1 = run[3], out1 = run[4];
+      const uint32_t D1 = Dsh[c1] & 0xffffu, E1 = Dsh[c1] >> 16;
+      if (t < nchunks && t >= c1 && (Dsh[t] & 0xffffu) <= D1) {
+        const uint32_t i = D1 - (Dsh[t] & 0xffffu), et = np1 + E1 - (Dsh[t] >> 16);
+        bool on = false;
+        uint32_t Ot = O1, ot = out1;
         if (i == 0) {
-          if (t == c1) put(np1, {y1, Esh[c1], O1, out1});
+          if (t == c1) {
+            put(np1, {y1, Esh[c1], O1, out1});
+            on = true;
+          }
         } else {
           const uint32_t p = lift(c1, i - 1);
-          if (J[0][p] == t && p != t) put(np1 + i, {Esh[p], Esh[t], O1 + out1 + SSsh[c1] - SSsh[p], Wsh[p]});
+          if (J[0][p] == t && p != t) {
+            const uint32_t np_ = Lsh[p];
+            const uint32_t yt = np_ ? drec0(p, np_ - 1).y : Esh[p];
+            Ot = O1 + out1 + SSsh[c1] - SSsh[p] + Wdsh[p];
+            ot = Wsh[p];
+            put(et, {yt, Esh[t], Ot, ot});
+            on = true;
+          }
+        }
+        if (on && J[0][t] != t) {  // (a root's deep elements are the serial chain's)
+          uint32_t Ok = Ot + ot;
+          for (uint32_t k = 0; k < Lsh[t]; ++k) {
+            const uint4 dr = drec0(t, k);
+            put(et + 1 + k, {dr.x, dr.y, Ok, dr.z});
+            Ok += dr.z;
+          }
         }
       }
       if (w0) {  // wave 0 goes on after the run's last element
         const uint32_t root = lift(c1, D1);
-        np = np1 + D1 + 1;
+        np = np1 + E1 + 1;
         O = (uint64_t)O1 + out1 + SSsh[c1];
         y = Esh[root];
         cprev = root;
@@ -1601,6 +1664,7 @@ __global__ __launch_bounds__(kChainThreads) void k_stream_chain(const uint8_t* _
     ctl[1] = bad;
   }
   if (lane >= 2 && lane < 4 + nrounds) ctl[lane] = 0;  // the fill's flag and the resolve counters
+#undef drec0
 }
 
 // k_origin_fill for the device chain's path: elements past ctl[0] exit; a failing element sets ctl[2]
