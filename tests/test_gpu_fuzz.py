@@ -124,3 +124,33 @@ def test_single_calls_random_structured_inputs(sm, oracle, gpu_available, seed):
                 assert sm.uncompress(split) == raw
     finally:
         sm.set_split_compress(True)
+
+
+@pytest.mark.parametrize("seed", range(1, 1 + int(os.environ.get("SM_FUZZ_SEEDS", "3"))))
+def test_small_path_foreign_streams(sm, oracle, gpu_available, seed):
+    """Path 4 (sm_api.hip small_uncompress: index, parallel-run chain, fill, resolve) on seeded
+    foreign streams -- literal/copy mixes with no 64 KiB block structure, from copy-heavy (512-byte
+    index chunks) to literal-heavy (1 KiB chunks, deep entries), copy-4 offsets, 1-byte copies --
+    and on single-byte mutations of them: output and status equal the oracle's."""
+    from streams import build, random_ops
+    rng = np.random.default_rng(4000 + seed)
+    for _ in range(8):
+        target = int(rng.integers(5_000, 1_200_000))
+        ops = random_ops(rng, target, max_lit=int(rng.choice([8, 60, 300, 2000])),
+                         max_off=int(rng.choice([4096, 65535, 300_000])),
+                         long_lit_p=float(rng.choice([0.0, 0.02, 0.2])), near=int(rng.choice([64, 4096])))
+        s, e = build(ops)
+        assert oracle.uncompress(s) == e
+        assert sm.uncompress(s) == e, len(e)
+        for _ in range(3):
+            bad = bytearray(s)
+            bad[int(rng.integers(2, len(bad)))] = int(rng.integers(0, 256))
+            bad = bytes(bad)
+            st_o, out_o = oracle.uncompress_status(bad)
+            try:
+                st_g, out_g = 0, sm.uncompress(bad)
+            except sm.SnappyError as exc:
+                st_g, out_g = exc.code, None
+            assert st_g == st_o
+            if st_o == 0:
+                assert out_g == out_o
