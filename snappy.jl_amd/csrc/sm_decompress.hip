@@ -822,13 +822,45 @@ template <uint32_t kC>  // (the chunk size: lim - p <= kC)
 __device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint64_t p, uint64_t lim, uint16_t* jt,
                                 uint32_t lane, uint8_t* stg, uint64_t& exit_pos, uint64_t& produced) {
   constexpr uint32_t kStage = kC + kIdxPad;
+  uint64_t o = 0;
+  {  // Quick path: up to kQuickTags tags decoded one by one from a single load of the 256 bytes
+     // at p's dword (zero past N, as the stage), no staging and no window walk.  A deep entry a
+     // few bytes before its chunk's end, or one soon followed by a long literal, then costs one
+     // round trip (most deep levels and walks of literal-heavy streams: paper-100k.pdf).
+    constexpr uint32_t kQuickTags = 8;
+    const uint32_t base = (uint32_t)p & ~3u;
+    const uint32_t w = load_word(in, N, base + 4 * lane);
+    uint64_t q = p, oq = 0;
+    for (uint32_t k = 0; k < kQuickTags && q < lim; ++k) {
+      const uint64_t rel = q - base;
+      if (rel + 12 > 4 * kWave) break;
+      const uint32_t i = (uint32_t)rel >> 2, sh = (uint32_t)rel & 3u;
+      const uint32_t w0 = readlane(w, i), w1 = readlane(w, i + 1), w2 = readlane(w, i + 2);
+      const uint32_t c = __builtin_amdgcn_alignbyte(w1, w0, sh) & 0xff;
+      const uint32_t tr = __builtin_amdgcn_alignbyte(w2, w1, sh) << 24 | (__builtin_amdgcn_alignbyte(w1, w0, sh) >> 8);
+      const uint32_t entry = char_entry(c);
+      const uint32_t taglen = entry >> 11;
+      const uint32_t trailer = taglen >= 4 ? tr : (tr & ((1u << (8 * taglen)) - 1u));
+      if (c & 3) {
+        q += 1 + taglen;
+        oq += entry & 0xff;
+      } else {
+        const uint32_t lit = (entry & 0xff) + trailer;  // u32 wrap, as the reference
+        q += 1ull + taglen + lit;
+        oq += lit;
+      }
+    }
+    p = q;  // (the window walk goes on from here when the quick path did not leave)
+    o = oq;
+  }
   const uint64_t sp = p;
-  stage_bytes(stg, in, N, (uint32_t)sp, kStage, lane);
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: its LDS stores land before its loads)
+  if (p < lim) {
+    stage_bytes(stg, in, N, (uint32_t)sp, kStage, lane);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);  // (one wave: its LDS stores land before its loads)
+  }
   auto rd8 = [&](uint64_t x) -> uint64_t {
     return x >= sp && x - sp + 8 <= kStage ? lds_ld64(stg, (uint32_t)(x - sp)) : load8z(in, N, (uint32_t)x);
   };
-  uint64_t o = 0;
   while (p < lim) {
     const uint32_t rlim = (uint32_t)min((uint64_t)256, lim - p);
     uint32_t cpos, csz, sizes;
