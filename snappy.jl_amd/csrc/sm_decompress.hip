@@ -1397,14 +1397,17 @@ __device__ inline uint32_t rec_compact(uint2 r, uint64_t base) {
 // The chain, in parallel where it can be.  Chunk c's lane-0 walk exits at E(c); entered anywhere,
 // its walk usually meets lane 0's path and exits there too.  The link c -> c' holds when E(c)
 // enters c' at an entry the records cover (offset < kIdxEntries) AND that entry's walk exits at
-// E(c') -- then the element after the one in c' is again decided by a link.  Pointer jumping over
-// the links (one thread per chunk, kLift rounds) gives every chunk its distance D to the end of
-// its links, the output SS on the way, and the jump tables J[k] (2^k links).  When the serial
-// chain (wave 0) stands on an entry whose walk exits at E(c1) with D(c1) >= kMinRun links ahead,
-// every chunk t tests in parallel whether it lies i = D(c1) - D(t) links along from c1 (J0 of the
-// node i - 1 along is t) and writes its own path element; wave 0 continues after the last.
-// Every run element is one the serial chain would take (same record, same exit), so the path is
-// identical; anything else (deep entries, walks, records not in LDS) stays serial.
+// E(c') -- then the element after the one in c' is again decided by a link.  A link may also pass
+// through chain 0's deep records of c first (E(c) deep in a later chunk, consecutive long
+// literals: the deep elements the serial chain would take there).  Pointer jumping over the
+// links (one thread per chunk, kLift rounds) gives every chunk its distance D to the end of its
+// links, the elements and the output (SS) on the way, and the jump tables J[k] (2^k links).
+// When the serial chain (wave 0) stands on an entry whose walk exits at E(c1) with D(c1) >=
+// kMinRun links ahead, every chunk t tests in parallel whether it lies i = D(c1) - D(t) links
+// along from c1 (J0 of the node i - 1 along is t) and writes its own path element and its link's
+// deep elements; wave 0 continues after the last.  Every run element is one the serial chain
+// would take (same record, same exit), so the path is identical; anything else (other deep
+// entries, walks) stays serial.
 __device__ inline uint4 chain_deep0(const uint4* sdeep, const uint4* __restrict__ deep, uint32_t nsdeep, uint32_t c,
                                     uint32_t k) {
   const uint32_t i = kDeepLevels * kDeepChains * c + k;
