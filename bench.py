@@ -215,6 +215,13 @@ class StreamShard:
         self.status = torch.zeros(nf, dtype=torch.int32, device=dev)
         self.offsets = None
         self.stream_len = None
+        # the rank's byte range of the stream, materialised (sm_place_fragments_device): rank 0's
+        # starts with the varint header; capacity = the worst case of its fragments
+        self.header = lo == 0
+        cap = int(sum(32 + int(x) + int(x) // 6 for x in lens)) + (5 if self.header else 0)
+        self.d_stream = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
+        self.loc_off = torch.zeros(max(nf, 1), dtype=torch.int64, device=dev)[:nf]
+        self.place_status = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def compress(self, sm):
         sm.compress_fragments_device(self.d_in, self.in_off, self.in_len, self.d_comp, self.comp_off, self.comp_len,
@@ -223,8 +230,21 @@ class StreamShard:
     def index(self, dist_mod, rank, world):
         self.offsets, self.stream_len = dist_mod.stream_offsets_device(self.comp_len, self.total, rank, world)
 
+    def place(self, sm):
+        """This rank's fragments at their global offsets (minus its range's start) in d_stream."""
+        sm.place_fragments_device(self.d_comp, self.comp_off, self.comp_len, self.offsets, self.d_stream, self.total,
+                                  self.header, d_local_off=self.loc_off, d_status=self.place_status)
+
+    def range_bytes(self):
+        """Bytes of this rank's materialised range (rank 0: the header included)."""
+        import torch
+        if self.nfrag == 0:
+            return len_varint(self.total) if self.header else 0
+        return int((self.loc_off[-1] + self.comp_len[-1].to(torch.int64)).item())
+
     def uncompress(self, sm):
-        sm.uncompress_fragments_device(self.d_comp, self.comp_off, self.comp_len, self.d_dec, self.in_off,
+        """The fragments decoded where they were placed: out of the materialised stream range."""
+        sm.uncompress_fragments_device(self.d_stream, self.loc_off, self.comp_len, self.d_dec, self.in_off,
                                        self.in_len, self.dec_len, self.status)
 
     def verify(self, sm):
@@ -236,10 +256,19 @@ class StreamShard:
         # the global index: a real stream length (not poisoned by an error mark, dist.py), and
         # offsets strictly increasing by this rank's sizes
         ok = ok and self.stream_len is not None and int(self.stream_len.item()) > 0
+        ok = ok and int(self.place_status.item()) == 0
         if self.nfrag > 1 and self.offsets is not None:
             d = self.offsets[1:] - self.offsets[:-1]
             ok = ok and bool(torch.equal(d, self.comp_len[:-1].to(torch.int64)))
         return ok
+
+
+def len_varint(v):
+    n = 1
+    while v >= 0x80:
+        v >>= 7
+        n += 1
+    return n
 
 
 _SM = None
@@ -320,6 +349,7 @@ ROCPROF_KERNELS = {
     "compress_fragments": ["sm::k_literal_screen", "sm::k_compress_sc<0>"],
     "uncompress": ["sm::k_decompress"],
     "uncompress_random": ["sm::k_decompress"],
+    "uncompress_reference_streams": ["sm::k_decompress"],
 }
 
 
@@ -565,11 +595,22 @@ def main():
     # byte-identical (reference) mode on the same batch: Snappy.jl's own bytes (tests/ check
     # them against the oracle block for block); reported beside the headline, not in it
     t_ref = kernel_ms(lambda: batch.compress(sm, "reference"), 3)
-    ref_mode = {"workload": "the headline's %d text blocks, byte-identical (reference) mode compress" % args.blocks,
+    ref_comp = batch.comp_bytes()
+    # config 3's other half: the decode of the reference-mode (Snappy.jl's own)
+    # streams of the same blocks, with its own roofline
+    t_rd = kernel_ms(lambda: batch.uncompress(sm), reps)
+    ref_mode = {"workload": "the headline's %d text blocks, byte-identical (reference) mode compress, and the "
+                            "uncompress of those streams (config 3's reference-mode inputs)" % args.blocks,
                 "compress_GBps": round(in_bytes / (t_ref * 1e-3) / 1e9, 3),
-                "ratio": round(batch.comp_bytes() / in_bytes, 5),
+                "ratio": round(ref_comp / in_bytes, 5),
                 "roundtrip_bit_exact": batch.verify()}
     ok_all &= ref_mode["roundtrip_bit_exact"]
+    ref_streams = {"workload": "config 3: uncompress of the %d reference-mode (Snappy.jl byte-identical) streams of "
+                               "the headline blocks, the stream set the oracle produces" % args.blocks,
+                   "reference_streams_uncompress_GBps": round(in_bytes / (t_rd * 1e-3) / 1e9, 3),
+                   "ratio": round(ref_comp / in_bytes, 5),
+                   "roundtrip_bit_exact": ref_mode["roundtrip_bit_exact"],
+                   "roofline": roofline("uncompress_reference_streams", ref_comp + in_bytes, t_rd)}
     batch.compress(sm, "fast")
 
     extras = {}
@@ -619,28 +660,49 @@ def main():
         def lstep():
             sh.compress(sm)
             sh.index(dmod, rank, world)
+            sh.place(sm)
             sh.uncompress(sm)
         l_el = timed_steps(lstep, args.steps, args.warmup, world, dist, dev)
         sh.index(dmod, rank, world)
+        sh.place(sm)
         lt_c = kernel_ms(lambda: sh.compress(sm), reps)
+        lt_p = kernel_ms(lambda: sh.place(sm), reps)
         lt_d = kernel_ms(lambda: sh.uncompress(sm), reps)
         l_ok = sh.verify(sm)
-        ok_all &= l_ok
         lc_local = int(sh.comp_len.to(torch.int64).sum())
-        stream_len = int(sh.stream_len.item())
+        # the stream's length read back from the materialised ranges (summed over ranks), which
+        # must equal the all-gathered index's total
+        rb = torch.tensor([sh.range_bytes()], dtype=torch.int64, device=dev)
+        if dist is not None:
+            dist.all_reduce(rb)
+        stream_len = int(rb.item())
+        l_ok = l_ok and stream_len == int(sh.stream_len.item())
+        stream_sha = None
+        if world == 1:  # the whole stream is rank 0's range: decode it through the single-buffer API
+            import hashlib
+            host = sh.d_stream[:stream_len].cpu().numpy()
+            stream_sha = hashlib.sha256(host.tobytes()).hexdigest()
+            back = sm.uncompress(host.tobytes())
+            l_ok = l_ok and back == big.tobytes()
+            del host, back
+        ok_all &= l_ok
         per_rank_ms = l_el / args.steps * 1e3
         large = {
             "workload": "config 5: one %d-B (644 MiB) stream = %d fragments, %d..%d per GPU (contiguous shards); "
                         "per step: fast-mode fragment compress + RCCL all-gather of the u32 fragment sizes + "
-                        "offset scan + fragment uncompress" % (big.size, nfrag, nfrag // world,
-                                                                (nfrag + world - 1) // world),
+                        "offset scan + the fragments placed at their stream offsets (sm_place_fragments_device; "
+                        "rank 0 writes the varint header) + uncompress of the placed fragments"
+                        % (big.size, nfrag, nfrag // world, (nfrag + world - 1) // world),
             "scaling": "strong",
             "GBps": round(2.0 * big.size * args.steps / l_el / 1e9, 3),
             "ms_per_step": round(per_rank_ms, 4),
             "fragments_rank0": hi - lo,
             "compress_GBps_per_gpu": round(sh.in_bytes / (lt_c * 1e-3) / 1e9, 3),
             "uncompress_GBps_per_gpu": round(sh.in_bytes / (lt_d * 1e-3) / 1e9, 3),
+            "place_GBps_per_gpu": round(2 * lc_local / (lt_p * 1e-3) / 1e9, 3),
             "stream_bytes": stream_len,
+            "stream_bytes_source": "the materialised ranges' lengths summed over ranks (= the gathered index total)",
+            "stream_sha256": stream_sha,
             "ratio": round(stream_len / big.size, 5),
             "roundtrip_bit_exact": l_ok,
             "roofline": roofline("compress_fragments", sh.in_bytes + lc_local + 4 * sh.nfrag, lt_c),
@@ -704,6 +766,8 @@ def main():
             "random": rnd,
             "large": large,
             "reference_mode": ref_mode,
+            "reference_streams_uncompress_GBps": ref_streams["reference_streams_uncompress_GBps"],
+            "reference_streams": ref_streams,
             "cpu_baseline": cpu,
         }
         line.update(extras)
@@ -716,7 +780,8 @@ def main():
 
 
 def extra_modes(sm, batch, in_bytes):
-    """--extras: dense mode, decode of the reference-mode streams, validation."""
+    """--extras: dense mode and its streams' decode, validation (the reference-mode streams'
+    decode is in the default line: `reference_streams`)."""
     import torch
     out = {}
     t_dc = kernel_ms(lambda: batch.compress(sm, "dense"), 5)
@@ -730,11 +795,6 @@ def extra_modes(sm, batch, in_bytes):
     t_v = kernel_ms(lambda: sm.validate_batch_device(batch.d_comp, batch.comp_off, batch.comp_len, vst), 5)
     out["validate_GBps"] = round(in_bytes / (t_v * 1e-3) / 1e9, 3)
     out["validate_ok"] = int(vst.abs().sum()) == 0
-    batch.compress(sm, "reference")  # (its compress rate is in the line's reference_mode)
-    t_rd3 = kernel_ms(lambda: batch.uncompress(sm), 5)
-    out["reference_streams_uncompress_GBps"] = round(in_bytes / (t_rd3 * 1e-3) / 1e9, 3)
-    out["reference_ok"] = batch.verify()
-    batch.compress(sm, "fast")
     return out
 
 

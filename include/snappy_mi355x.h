@@ -134,6 +134,25 @@ sm_status sm_compress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const u
                                        const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                        const uint64_t* d_out_off, uint32_t* d_out_len, uint64_t total_len,
                                        int mode, void* stream);
+/* Places fragments of ONE stream at their offsets in it -- the concatenation of src/Snappy.jl:29-35
+ * (fragment i's bytes follow fragment i-1's behind varint(total)) for a stream whose fragments were
+ * compressed in shards, e.g. one contiguous shard per GPU (snappy.jl_amd/dist.py).
+ * Fragment b, d_len[b] bytes at d_src + d_src_off[b] (sm_compress_fragments_device's output), is
+ * copied to d_dst + (d_dst_off[b] - base), where d_dst_off[b] is its offset in the whole stream
+ * (the exclusive scan of all fragments' sizes behind the header) and
+ *   write_header != 0: base = 0 -- d_dst is the stream from its first byte, and varint(total_len)
+ *                      is written at d_dst[0..] (the shard holding fragment 0);
+ *   write_header == 0: base = d_dst_off[0] -- d_dst is this caller's byte range of the stream,
+ *                      starting at its first fragment.
+ * d_dst has room for dst_capacity bytes.  d_local_off (optional, nfrag u64) receives
+ * d_dst_off[b] - base (the fragments' offsets in d_dst, for sm_uncompress_fragments_device).
+ * A length that is an error mark (>= SM_OUT_LEN_ERROR), or a fragment that would end past
+ * dst_capacity, copies nothing and sets *d_status = SM_ERR_DEVICE (optional; never cleared: zero
+ * it first).  Asynchronous on `stream`. */
+sm_status sm_place_fragments_device(sm_ctx* ctx, const uint8_t* d_src, const uint64_t* d_src_off,
+                                    const uint32_t* d_len, uint32_t nfrag, const uint64_t* d_dst_off,
+                                    uint64_t total_len, int write_header, uint8_t* d_dst, uint64_t dst_capacity,
+                                    uint64_t* d_local_off, int32_t* d_status, void* stream);
 /* Fragments of ONE stream, decoded (the inverse of sm_compress_fragments_device; the block loop
  * of src/Snappy.jl:46-52 over src/internal.jl:411-466 without the varint header): fragment b is
  * d_in[d_in_off[b] .. +d_in_len[b]) and must decode to exactly d_frag_len[b] (<= 65536) bytes at

@@ -47,7 +47,7 @@ ABI_SYMBOLS = (
     "sm_ctx_set_split_compress", "sm_ctx_last_compress_split",
     "sm_find_match_length", "sm_validate_batch_device", "sm_uncompressed_length_batch_device",
     "sm_validate_compressed_buffer", "sm_compress_batch_sharded", "sm_uncompress_batch_sharded",
-    "sm_uncompress_fragments_device", "sm_snappy_compress", "sm_snappy_uncompress",
+    "sm_uncompress_fragments_device", "sm_place_fragments_device", "sm_snappy_compress", "sm_snappy_uncompress",
     "sm_snappy_max_compressed_length", "sm_snappy_uncompressed_length", "sm_snappy_validate_compressed_buffer",
     "sm_snappy_set_mode",
 )
@@ -137,6 +137,9 @@ def load_library(path):
     L.sm_uncompressed_length_batch_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp]
     L.sm_validate_compressed_buffer.restype = i32
     L.sm_validate_compressed_buffer.argtypes = [vp, vp, sz]
+    L.sm_place_fragments_device.restype = i32
+    L.sm_place_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, ctypes.c_uint64, ctypes.c_int, vp,
+                                            ctypes.c_uint64, vp, vp, vp]
     L.sm_uncompress_fragments_device.restype = i32
     L.sm_uncompress_fragments_device.argtypes = [vp, vp, vp, vp, u32, vp, vp, vp, vp, vp, vp]
     # snappy-c.h shape (test/libsnappy.jl:5-30): (char*, size_t, char*, size_t*) -> int
@@ -435,6 +438,27 @@ def uncompress_batch_device(d_in, d_in_off, d_in_len, d_out, d_out_off, d_out_ca
     st = lib().sm_uncompress_batch_device(context(dev), _ptr(d_in), _ptr(d_in_off), _ptr(d_in_len),
                                           d_in_len.numel(), _ptr(d_out), _ptr(d_out_off), _ptr(d_out_cap),
                                           _ptr(d_out_len), _ptr(d_status), ctypes.c_void_p(stream))
+    if st:
+        raise SnappyError(st)
+
+
+def place_fragments_device(d_src, d_src_off, d_len, d_dst_off, d_dst, total_len, write_header, d_local_off=None,
+                           d_status=None, stream=None, device=None):
+    """Fragments of ONE stream at their offsets in it (sm_place_fragments_device): fragment b
+    (d_len[b] bytes at d_src + d_src_off[b]) to d_dst + d_dst_off[b] - base, base = 0 with
+    write_header (d_dst is the stream from byte 0; varint(total_len) is written there) or
+    d_dst_off[0] (d_dst is this shard's byte range).  d_local_off (int64, optional) receives the
+    fragments' offsets in d_dst; d_status (int32[1], optional, zeroed by the caller) turns
+    SM_ERR_DEVICE on an error-mark length or a fragment past d_dst's end."""
+    dev = d_dst.device.index if device is None else device
+    nfrag = d_len.numel()
+    nul = ctypes.c_void_p(0)
+    st = lib().sm_place_fragments_device(context(dev), _ptr(d_src) if nfrag else nul, _ptr(d_src_off) if nfrag else nul,
+                                         _ptr(d_len) if nfrag else nul, nfrag, _ptr(d_dst_off) if nfrag else nul,
+                                         int(total_len), 1 if write_header else 0, _ptr(d_dst), d_dst.numel(),
+                                         _ptr(d_local_off) if d_local_off is not None else nul,
+                                         _ptr(d_status) if d_status is not None else nul,
+                                         ctypes.c_void_p(_stream(stream, dev)))
     if st:
         raise SnappyError(st)
 

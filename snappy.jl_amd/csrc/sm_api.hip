@@ -705,6 +705,21 @@ sm_status sm_compress_fragments_device(sm_ctx* ctx, const uint8_t* d_in, const u
   return SM_OK;
 }
 
+sm_status sm_place_fragments_device(sm_ctx* ctx, const uint8_t* d_src, const uint64_t* d_src_off,
+                                    const uint32_t* d_len, uint32_t nfrag, const uint64_t* d_dst_off,
+                                    uint64_t total_len, int write_header, uint8_t* d_dst, uint64_t dst_capacity,
+                                    uint64_t* d_local_off, int32_t* d_status, void* stream) {
+  if (!ctx) return SM_ERR_ARGUMENT;
+  if (total_len > 0xffffffffull) return SM_ERR_INPUT_TOO_LARGE;  // src/Snappy.jl:21
+  if (nfrag == 0 && !write_header) return SM_OK;
+  if (!d_dst || (nfrag && (!d_src || !d_src_off || !d_len || !d_dst_off))) return SM_ERR_ARGUMENT;
+  if (write_header && dst_capacity < sm::varint_len((uint32_t)total_len)) return SM_BUFFER_TOO_SMALL;
+  DeviceGuard g(ctx->device);
+  SM_CHECK(sm::launch_place(d_src, d_src_off, d_len, d_dst_off, nfrag, total_len, write_header ? 1 : 0, dst_capacity,
+                            d_dst, d_local_off, d_status, (hipStream_t)stream));
+  return SM_OK;
+}
+
 sm_status sm_uncompress_batch_device(sm_ctx* ctx, const uint8_t* d_in, const uint64_t* d_in_off,
                                      const uint32_t* d_in_len, uint32_t nblk, uint8_t* d_out,
                                      const uint64_t* d_out_off, const uint32_t* d_out_cap,

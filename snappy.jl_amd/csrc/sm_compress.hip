@@ -10,15 +10,13 @@
 //
 // Data layout in HBM: input blocks at in[in_off[b]], outputs at out[out_off[b]] (caller
 // reserves max_compressed_length(len)+5 per block, i.e. fixed slots), out_len[b] = bytes.
+#include <type_traits>
+
 #include "sm_device.h"
 #include "sm_internal.h"
 
 namespace sm {
 
-#if SM_STAMP
-__device__ unsigned long long g_stamp_x[8];
-#endif
-STAMP_MACROS(8)
 
 // ---- output emission (global memory, wave-uniform op) -------------------------------
 
@@ -103,6 +101,18 @@ struct BlockBytes {
   __device__ uint32_t byte(uint32_t pos) const { return __builtin_amdgcn_raw_buffer_load_b8(r, (int)pos, 0, 0); }
 };
 
+// The block staged in LDS (one parse per CU, for single calls and small batches): the same bytes
+// as BlockBytes -- exact below n, 0 at and past n (the staging zeroes 32 bytes past n, and a
+// position past n is clamped to n) -- at LDS latency instead of L2/HBM latency on the parse's
+// dependency chain (a lone 64 KiB fragment's parse is that chain: ~2 loads per probe step).
+struct LdsBytes {
+  const uint8_t* blk;
+  uint32_t n;
+  __device__ uint32_t word(uint32_t pos) const { return lds_ld32(blk, min(pos, n)); }
+  __device__ uint32_t byte(uint32_t pos) const { return blk[min(pos, n)]; }
+};
+constexpr uint32_t kLdsBlockPad = 32;
+
 // Table entry h is half (h & 1) of dword h >> 1 and holds a position, 0 when never written.
 // The reference stores pos - 1 with 0xffff = empty and reads candidate (entry + 1) mod 2^16
 // (Snappy.jl:30, internal.jl:190-191): the same candidates, position 0 and "empty" alike
@@ -122,7 +132,8 @@ __device__ inline uint32_t tab_probe(uint32_t* t, uint32_t h, uint32_t p) {
 }
 
 // wave-cooperative copy of len block bytes from s to global memory (16-byte stores in the body)
-__device__ inline void copy_to_global(const BlockBytes& S, uint8_t* __restrict__ g, uint32_t s, uint32_t len,
+template <class B>
+__device__ inline void copy_to_global(const B& S, uint8_t* __restrict__ g, uint32_t s, uint32_t len,
                                       uint32_t lane) {
   uint32_t head = (uint32_t)((16 - ((uintptr_t)g & 15)) & 15);
   if (head > len) head = len;
@@ -149,7 +160,8 @@ __device__ inline void copy_to_global(const BlockBytes& S, uint8_t* __restrict__
 }
 
 // internal.jl:252-287, whole wave.  Q3: the one-byte tag only for len < 60.
-__device__ inline uint32_t emit_literal_w(const BlockBytes& S, uint8_t* dst, uint32_t op, uint32_t start,
+template <class B>
+__device__ inline uint32_t emit_literal_w(const B& S, uint8_t* dst, uint32_t op, uint32_t start,
                                           uint32_t len, uint32_t lane) {
   const uint32_t n = len - 1;
   if (len < 60) {
@@ -168,7 +180,8 @@ __device__ inline uint32_t emit_literal_w(const BlockBytes& S, uint8_t* dst, uin
 // Emission of ntok (<= 64) queued copies: lane t holds copy t (tk = position | offset << 16,
 // tl = length), preceded by its literal run from the previous copy's end (`base` for t = 0).
 // Returns the new output offset; base becomes the last copy's end.
-__device__ uint32_t flush_copies(const BlockBytes& S, uint8_t* __restrict__ dst, uint32_t op, uint32_t& base,
+template <class B>
+__device__ uint32_t flush_copies(const B& S, uint8_t* __restrict__ dst, uint32_t op, uint32_t& base,
                                  uint32_t ntok, uint32_t tk, uint32_t tl, uint32_t lane) {
   const bool act = lane < ntok;
   const uint32_t pos = tk & 0xffffu, off = tk >> 16;
@@ -217,8 +230,14 @@ __device__ inline uint32_t writelane(uint32_t v, uint32_t l, uint32_t old) {
   return old;
 }
 
+// kLds = false: the block read in place from HBM (BlockBytes), five parses per CU -- batches;
+// kLds = true: the block staged in LDS (LdsBytes), one parse per CU -- at most one block per CU
+// (single calls: alice29.txt's 64 KiB fragments 4.95 ms -> see DESIGN.md section 3.1).  The
+// parse below is the same code for both, so the bytes are identical.
+template <bool kLds>
 __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t stab[kTabBytes / 4];
+  __shared__ __attribute__((aligned(16))) uint8_t sblk[kLds ? kBlockSize + kLdsBlockPad : 16];
 
   const uint32_t b = blockIdx.x;
   const uint32_t lane = lane_id();
@@ -228,9 +247,17 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
     if (lane == 0) a.out_len[b] = 0xffffffffu;
     return;
   }
-  BlockBytes S;
-  S.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.in + a.in_off[b]), (short)0, (int)n, 0x00020000);
-  S.nm4 = n - 4;
+  std::conditional_t<kLds, LdsBytes, BlockBytes> S;
+  if constexpr (kLds) {
+    const uint8_t* src = a.in + a.in_off[b];
+    wave_load_global_to_lds(sblk, src, n, lane);
+    for (uint32_t k = n + lane; k < n + kLdsBlockPad; k += kWave) sblk[k] = 0;  // zeros past the block
+    S.blk = sblk;
+    S.n = n;
+  } else {
+    S.r = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.in + a.in_off[b]), (short)0, (int)n, 0x00020000);
+    S.nm4 = n - 4;
+  }
   const uint32_t tsize = a.table_size ? a.table_size : hashtable_size(n);      // Snappy.jl:27 (Q2)
   const uint32_t shift = 32 - (31 - __builtin_clz(tsize));                     // internal.jl:128
   for (uint32_t k = lane; k < tsize / 2; k += kWave) stab[k] = 0;              // Snappy.jl:30
@@ -261,11 +288,9 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
   const uint32_t e = n - 1;                  // inclusive end (ip_end)
   const int32_t ip_limit = (int32_t)n - 16;  // internal.jl:131, Q1: 1-based ip_end-15
   uint32_t ip = 0, next_emit = 0, base = 0, ntok = 0, tk = 0, tl = 0;
-  STAMP_DECL
 
   if (n >= kInputMarginBytes) {                                                // internal.jl:133
     for (;;) {
-      STAMP(4)
       ip += 1;                                                                 // :163
       // literal search, 64 probes per step (:167-194)
       const uint32_t p0 = ip;
@@ -275,7 +300,6 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
       uint64_t hm = 0;
 #pragma unroll
       for (uint32_t i = 0; i < kProbeSteps; ++i) {
-        STAMP_COUNT(7, 1)
         p = p0 + Dk[i];
         valid = (int32_t)(p0 + Dn[i]) <= ip_limit;                             // :175
         const uint32_t cur = S.word(p);
@@ -297,7 +321,6 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         ip = pj;
         cand = readlane(raw, j);
       }
-      STAMP(0)
       if (__builtin_expect(!found, 0)) break;                                  // -> remainder
       for (;;) {                                                               // :211-239
         // bytes [0, 4) of a round are the verification (:238; known equal after a probe hit),
@@ -329,11 +352,9 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
             }
           }
         }
-        STAMP(2)
         // :238; cand >= ip (a later position, only if the table's insert order broke) fails as a
         // verification does: the guard the lane-order assumption lacked
         if (__builtin_expect(f < 4 || cand >= ip, 0)) break;
-        STAMP_COUNT(6, 1)
         // The next candidate first (:228-235, one lane: insert ip-1, read and replace the entry
         // for ip), so the bookkeeping below runs under its LDS round trip.  Past ip_limit the
         // inserts are never read: the parse ends there.
@@ -360,22 +381,17 @@ __global__ __launch_bounds__(64) void k_compress_exact(CompressArgs a) {
         ip = ipn;
         next_emit = ip;
         if (__builtin_expect(ntok == kWave, 0)) {
-          STAMP(3)
           op = flush_copies(S, dst, op, base, ntok, tk, tl, lane);
           ntok = 0;
-          STAMP(1)
         }
         if (__builtin_expect((int32_t)ip >= ip_limit, 0)) break;               // :222
         cand = readlane(raw, 0);
-        STAMP(3)
       }
       if (__builtin_expect((int32_t)ip >= ip_limit, 0)) break;                 // :222 -> remainder
     }
   }
   if (ntok) op = flush_copies(S, dst, op, base, ntok, tk, tl, lane);
   if (next_emit <= e) op = emit_literal_w(S, dst, op, next_emit, e - next_emit + 1, lane);  // :244-248
-  STAMP(5)
-  STAMP_FLUSH(g_stamp_x)
   if (lane == 0) a.out_len[b] = op;
 }
 
@@ -526,6 +542,51 @@ __global__ __launch_bounds__(256) void k_gather_parts(const uint8_t* __restrict_
   }
 }
 
+// ---- a sharded stream's fragments at their places in it (Snappy.jl:29-35) ----------
+// Fragment b (len[b] bytes at src + src_off[b]) to dst + (dst_off[b] - base): dst_off[b] is the
+// fragment's offset in the whole stream (the all-gathered exclusive scan behind the varint
+// header), base = 0 with the header (dst is the stream from its first byte and varint(total) is
+// written there) or dst_off[0] without it (dst is the caller's byte range from its first
+// fragment).  loc_off[b] (optional) receives dst_off[b] - base.  A length that is an error mark,
+// or a fragment that would end past cap, copies nothing and sets *status = SM_ERR_DEVICE
+// (optional; never cleared here).  blockIdx.y strides the fragment's 16-byte units.
+__global__ __launch_bounds__(256) void k_place(const uint8_t* __restrict__ src, const uint64_t* src_off,
+                                               const uint32_t* len, const uint64_t* dst_off, uint32_t nfrag,
+                                               uint64_t total, int header, uint64_t cap, uint8_t* __restrict__ dst,
+                                               uint64_t* loc_off, int32_t* status) {
+  const uint32_t b = blockIdx.x;
+  if (header && b == 0 && blockIdx.y == 0) {  // varint(total), src/varint.jl:46-69
+    const uint32_t hv = varint_len((uint32_t)total);
+    if (threadIdx.x < hv && threadIdx.x < cap)
+      dst[threadIdx.x] = (uint8_t)((((uint32_t)total >> (7 * threadIdx.x)) & 0x7f) | (threadIdx.x + 1 < hv ? 0x80 : 0));
+  }
+  if (b >= nfrag) return;  // (an empty stream: the header alone)
+  const uint64_t base = header ? 0ull : dst_off[0];
+  const uint32_t n = len[b];
+  const uint64_t at = dst_off[b] - base;  // (a mark earlier in the scan wraps this past cap)
+  const bool bad = n >= kOutLenError || at > cap || cap - at < n;
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
+    if (loc_off) loc_off[b] = at;
+    if (bad && status) *status = kErrDevice;
+  }
+  if (bad) return;
+  const uint8_t* const s = src + src_off[b];
+  if (((uintptr_t)s & 15) == 0) {
+    gather_unit(s, n, dst + at, blockIdx.y, gridDim.y);
+  } else {
+    for (uint32_t k = blockIdx.y * blockDim.x + threadIdx.x; k < n; k += blockDim.x * gridDim.y) dst[at + k] = s[k];
+  }
+}
+
+hipError_t launch_place(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, const uint64_t* dst_off,
+                        uint32_t nfrag, uint64_t total, int header, uint64_t cap, uint8_t* dst, uint64_t* loc_off,
+                        int32_t* status, hipStream_t s) {
+  if (nfrag == 0 && !header) return hipSuccess;
+  hipLaunchKernelGGL(k_place, dim3(max(nfrag, 1u), 4), dim3(256), 0, s, src, src_off, len, dst_off, nfrag, total, header,
+                     cap, dst, loc_off, status);
+  return hipGetLastError();
+}
+
 hipError_t launch_frag_plan(uint64_t n, uint32_t nfrag, uint64_t slot, uint64_t* in_off, uint32_t* in_len,
                             uint64_t* out_off, hipStream_t s) {
   hipLaunchKernelGGL(k_frag_plan, dim3((nfrag + 255) / 256), dim3(256), 0, s, n, nfrag, slot, in_off, in_len, out_off);
@@ -550,21 +611,31 @@ hipError_t launch_frag_gather(const uint8_t* src, const uint64_t* src_off, const
   return hipGetLastError();
 }
 
-#if SM_STAMP
-extern "C" int sm_debug_stamps_x(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_x), sizeof(g_stamp_x)) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[8] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_x), z, sizeof(z)) != hipSuccess) return -1;
+
+// the current device's CU count (cached per device)
+static uint32_t cu_count() {
+  static uint32_t cache[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+  uint32_t ncu = __atomic_load_n(&cache[dev], __ATOMIC_RELAXED);
+  if (!ncu) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+    ncu = (uint32_t)v;
+    __atomic_store_n(&cache[dev], ncu, __ATOMIC_RELAXED);
   }
-  return 0;
+  return ncu;
 }
-#endif
 
 hipError_t launch_compress(const CompressArgs& a, int mode, hipStream_t s) {
   if (a.nblk == 0) return hipSuccess;
   if (mode != 0) return launch_compress_fast(a, mode, s);
-  hipLaunchKernelGGL(k_compress_exact, dim3(a.nblk), dim3(64), 0, s, a);
+  // at most one block per CU: each parse gets a CU and reads its block from LDS; more: five
+  // parses per CU reading their blocks in place (the LDS holds one staged block)
+  if (a.nblk <= cu_count())
+    hipLaunchKernelGGL(k_compress_exact<true>, dim3(a.nblk), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_compress_exact<false>, dim3(a.nblk), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

@@ -74,37 +74,6 @@ constexpr uint32_t kScMaxL = 255;         // longest copy token (u8 lengths)
 constexpr uint32_t kScSpinMax = 1u << SC_SPIN_BITS;  // hand-off polls (64+ cycles each) before a wait gives up
 static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, one 16-byte row");
 
-// Diagnostic builds only (-DSC_ABL=bits, tools/sc_abl.py): 1 no emission (G1, G2), 2 no resync
-// (first walks only), 4 no 16-byte choice between two full candidates, 8 no candidates (the
-// verify reads nothing), 16 no insert-token wait, 32 no writer copy-out, 64 no walks (every row
-// literals).  The output is not valid.
-#ifndef SC_ABL
-#define SC_ABL 0
-#endif
-// Diagnostic builds only (-DSC_DUP=bits, tools/pmc_dup.sh): an LDS instruction group issued twice
-// (the copy idempotent or its result unused), so the PMC deltas against the plain build give the
-// group's own LDS-array and bank-conflict cycles: 1 the insert exchanges (B), 2 the candidate
-// loads (C), 4 the walks' position loads, 8 the walks' candidate loads, 16 the walks' offset
-// reads (D), 32 the staging ors (G), 64 the hash step's loads (A).
-#ifndef SC_DUP
-#define SC_DUP 0
-#endif
-// Reads served from the block in HBM/L1 (a raw buffer over [0, n): unaligned, no bank
-// conflicts, the vector-memory pipe instead of the LDS): 1 the candidate checks (C), 2 the walks'
-// position bytes, 4 the walks' candidate bytes (D).  Measured (10K text blocks): 2 removes the
-// position bytes' 4-way bank conflict (row strides of 16 B: 58% of their LDS cycles,
-// profiles/r04_pmc_lds_attribution.json) but gains at most 1.5% (2.49 -> 2.45 ms in one A/B,
-// equal in the next); 1 and 4 put HBM/L1 latency on the walk's dependent chain (2.58 and
-// 2.50 ms).  Default 0: everything from the LDS copy.
-#ifndef SC_GC
-#define SC_GC 0
-#endif
-#ifndef SC_ORN  // 1: a literal piece ors only the dwords it reaches (2.049 -> 2.023 ms); 2: also its first
-#define SC_ORN 1  // dword and the copy tags' (per-dword branches: 2.063)
-#endif
-#ifndef SC_WPRE  // the writer reads the next slot's size word with this slot's bytes
-#define SC_WPRE 1
-#endif
 #ifndef SC_CB  // fast mode: section C's groups per batch of candidate loads in flight
 #define SC_CB 2
 #endif
@@ -124,10 +93,6 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #define SC_WSLEEP 1
 #endif
 
-#if SM_STAMP
-__device__ unsigned long long g_stamp_sc[12];
-#endif
-STAMP_MACROS(12)
 
 // per-wave LDS: rows of 16 positions (row r = lane r's positions)
 struct ScWaveLds {
@@ -167,17 +132,6 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_wait(uint32_t* p, P
   return v;
 }
 
-// (SC_DUP) the five dwords at LDS byte address wa (dword-aligned) read again, the result dropped
-__device__ inline void sc_dup5(uint32_t wa) {
-  uint64_t x, y;
-  uint32_t z;
-  asm volatile("ds_read2_b32 %0, %3 offset1:1\nds_read2_b32 %1, %3 offset0:2 offset1:3\nds_read_b32 %2, %3 offset:16\n"
-               "s_waitcnt lgkmcnt(0)" : "=v"(x), "=v"(y), "=v"(z) : "v"(wa) : "memory");
-}
-__device__ inline void sc_dup2(uint32_t wa) {
-  uint64_t x;
-  asm volatile("ds_read2_b32 %0, %1 offset1:1\ns_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(wa) : "memory");
-}
 
 __device__ inline uint32_t sc_ld32(const uint8_t* blk, uint32_t a) { return *reinterpret_cast<const uint32_t*>(blk + a); }
 
@@ -205,41 +159,6 @@ __device__ inline uint4 sc_ld128(const uint8_t* blk, uint32_t p) {
 __device__ inline uint32_t sc_diff8(uint32_t a0, uint32_t a1, uint32_t b0, uint32_t b1) {
   const uint64_t d = ((uint64_t)(a1 ^ b1) << 32) | (a0 ^ b0);
   return d ? (uint32_t)__builtin_ctzll(d) >> 3 : 8u;
-}
-
-// bytes v[0, len) (len 1..16) to the LDS byte array at byte address a (any alignment): masked ors
-// (ds_mskor_b32: D = (D & ~mask) | data), so lanes that share a dword do not race
-__device__ inline void sc_lds_put(uint32_t a, uint4 v, uint32_t len) {
-  const uint32_t sh = a & 3u, wa = a & ~3u;
-  // the len-byte mask as four dwords, then both shifted up by sh bytes into a 20-byte window
-  const uint32_t l0 = len >= 4 ? ~0u : (1u << (8 * len)) - 1;
-  const uint32_t l1 = len >= 8 ? ~0u : (len <= 4 ? 0u : (1u << (8 * (len - 4))) - 1);
-  const uint32_t l2 = len >= 12 ? ~0u : (len <= 8 ? 0u : (1u << (8 * (len - 8))) - 1);
-  const uint32_t l3 = len >= 16 ? ~0u : (len <= 12 ? 0u : (1u << (8 * (len - 12))) - 1);
-  uint32_t u[5], m[5];
-  if (sh == 0) {
-    u[0] = v.x, u[1] = v.y, u[2] = v.z, u[3] = v.w, u[4] = 0;
-    m[0] = l0, m[1] = l1, m[2] = l2, m[3] = l3, m[4] = 0;
-  } else {
-    const uint32_t r = 4 - sh;  // alignbyte(hi, lo, r) = (hi:lo) >> 8r
-    u[0] = v.x << (8 * sh), u[1] = __builtin_amdgcn_alignbyte(v.y, v.x, r), u[2] = __builtin_amdgcn_alignbyte(v.z, v.y, r);
-    u[3] = __builtin_amdgcn_alignbyte(v.w, v.z, r), u[4] = v.w >> (8 * r);
-    m[0] = l0 << (8 * sh), m[1] = __builtin_amdgcn_alignbyte(l1, l0, r), m[2] = __builtin_amdgcn_alignbyte(l2, l1, r);
-    m[3] = __builtin_amdgcn_alignbyte(l3, l2, r), m[4] = l3 >> (8 * r);
-  }
-  asm volatile("ds_mskor_b32 %0, %1, %2" : : "v"(wa), "v"(m[0]), "v"(u[0] & m[0]) : "memory");
-  if (m[1]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:4" : : "v"(wa), "v"(m[1]), "v"(u[1] & m[1]) : "memory");
-  if (m[2]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:8" : : "v"(wa), "v"(m[2]), "v"(u[2] & m[2]) : "memory");
-  if (m[3]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:12" : : "v"(wa), "v"(m[3]), "v"(u[3] & m[3]) : "memory");
-  if (m[4]) asm volatile("ds_mskor_b32 %0, %1, %2 offset:16" : : "v"(wa), "v"(m[4]), "v"(u[4] & m[4]) : "memory");
-}
-
-// the cs (2 or 3) low bytes of v to LDS byte address a, byte by byte (a copy tag: these bytes are
-// this lane's alone -- only a piece's first and last dword can be shared, and byte stores do not race)
-__device__ inline void sc_lds_put3(uint8_t* p, uint32_t v, uint32_t cs) {
-  p[0] = (uint8_t)v;
-  p[1] = (uint8_t)(v >> 8);
-  if (cs > 2) p[2] = (uint8_t)(v >> 16);
 }
 
 // v with the bytes from len (0..16) on cleared
@@ -277,21 +196,16 @@ __device__ inline void sc_lds_or(uint32_t a, uint4 v) {
   asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4\nds_or_b32 %0, %3 offset:8\nds_or_b32 %0, %4 offset:12\n"
                "ds_or_b32 %0, %5 offset:16"
                : : "v"(wa), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4) : "memory");
-  if (SC_DUP & 32)
-    asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4\nds_or_b32 %0, %3 offset:8\nds_or_b32 %0, %4 offset:12\n"
-                 "ds_or_b32 %0, %5 offset:16"
-                 : : "v"(wa), "v"(u0), "v"(u1), "v"(u2), "v"(u3), "v"(u4) : "memory");
 }
 
 // sc_lds_or for a piece of nb (1..16) bytes: the last three dwords only when the piece reaches
 // them (most literal runs are a few bytes: two ds_or_b32 instead of five)
 __device__ inline void sc_lds_orn(uint32_t a, uint4 v, uint32_t nb) {
-  if (!SC_ORN) return sc_lds_or(a, v);
   const uint32_t wa = (a - 1u) & ~3u, t = 0u - a, d = a - wa;  // (d: 1..4, the piece starts in dword 0 or 1)
   const uint32_t u0 = __builtin_amdgcn_alignbyte(v.x, 0u, t);
   const uint32_t u1 = __builtin_amdgcn_alignbyte(v.y, v.x, t);
-  if (SC_ORN < 2 || d < 4) asm volatile("ds_or_b32 %0, %1" : : "v"(wa), "v"(u0) : "memory");
-  if (SC_ORN < 2 || d + nb > 4) asm volatile("ds_or_b32 %0, %1 offset:4" : : "v"(wa), "v"(u1) : "memory");
+  asm volatile("ds_or_b32 %0, %1" : : "v"(wa), "v"(u0) : "memory");
+  asm volatile("ds_or_b32 %0, %1 offset:4" : : "v"(wa), "v"(u1) : "memory");
   if (d + nb > 8) {
     const uint32_t u2 = __builtin_amdgcn_alignbyte(v.z, v.y, t);
     const uint32_t u3 = __builtin_amdgcn_alignbyte(v.w, v.z, t);
@@ -305,13 +219,7 @@ __device__ inline void sc_lds_orn(uint32_t a, uint4 v, uint32_t nb) {
 __device__ inline void sc_lds_or3(uint32_t a, uint32_t cv, uint32_t cs = 3) {
   const uint32_t wa = (a - 1u) & ~3u, t = 0u - a;  // (as sc_lds_or)
   const uint32_t lo = __builtin_amdgcn_alignbyte(cv, 0u, t), hi = __builtin_amdgcn_alignbyte(0u, cv, t);
-  if (SC_ORN >= 2) {  // only the dwords the cs-byte tag reaches
-    if (a - wa < 4) asm volatile("ds_or_b32 %0, %1" : : "v"(wa), "v"(lo) : "memory");
-    if (a - wa + cs > 4) asm volatile("ds_or_b32 %0, %1 offset:4" : : "v"(wa), "v"(hi) : "memory");
-    return;
-  }
   asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
-  if (SC_DUP & 32) asm volatile("ds_or_b32 %0, %1\nds_or_b32 %0, %2 offset:4" : : "v"(wa), "v"(lo), "v"(hi) : "memory");
 }
 
 // v shifted up by t (0..3) bytes with the t-byte value tag below it
@@ -435,8 +343,7 @@ __device__ __attribute__((always_inline)) inline uint32_t sc_next_block(const Co
 // One super-chunk, by one wave (sections A-G2 above).
 template <int kDense>
 __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, const uint32_t k, const uint32_t n,
-                                                                   const uint32_t wave, const uint32_t lane_in,
-                                                                   const __amdgpu_buffer_rsrc_t gb) {
+                                                                   const uint32_t wave, const uint32_t lane_in) {
   // (the lane index laundered per super-chunk: otherwise the compiler hoists dozens of lane-derived
   // addresses out of the super-chunk loop, and the registers they hold serialise section C)
   uint32_t lane = lane_in;
@@ -444,7 +351,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   ScWaveLds& Wl = S.w[wave];
   const uint32_t sc0 = k * kScS, sce = min(sc0 + kScS, n);
   const uint32_t Tbase = lds_addr(S.T);
-  STAMP_DECL
   // ---- A. hashes of the 16 groups: LDS byte address of the bucket dword, the slot value ----
   // (group g's position is ql + 64 g: its dword address and byte shift are ql's plus a constant,
   // so the loads take immediate offsets; only the block's last super-chunk has positions whose 4
@@ -457,7 +363,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
 #pragma unroll
   for (int g = 0; g < (int)kScG; ++g) {
     const uint32_t w = sc_abyte(sc_ld32(S.blk, qa + 64 * g + 4), sc_ld32(S.blk, qa + 64 * g), qb);
-    if (SC_DUP & 64) sc_dup2(lds_addr(S.blk + qa + 64 * g));
     wq[g] = w;
     ha[g] = Tbase + 4 * sc_hash_bucket(w);
     hvv[g] = (g & 1) ? hv1 + ((64u * g) << 16) : hv0 + 64u * g;
@@ -468,18 +373,15 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     for (int g = 0; g < (int)kScG; ++g) ha[g] = ql + 64 * g + 4 <= n ? ha[g] : Tbase + 4 * kScTabWords;
   }
   const uint32_t mk0 = 0xffffu, mk1 = 0xffff0000u;
-  STAMP(0)
-  STAMP_COUNT(11, 1)
   // ---- B. the insert token: 16 masked exchanges in position order, then hand it on ----
   __builtin_amdgcn_s_setprio(SC_TPRIO);
-  for (uint32_t it = 0; !(SC_ABL & 16) && uniform(__hip_atomic_load(&S.ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != k; ++it) {
+  for (uint32_t it = 0; uniform(__hip_atomic_load(&S.ins, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != k; ++it) {
     if (it > kScSpinMax) {  // never expected: a broken hand-off must not hang the GPU
       S.err |= 1;  // (the insert token)
       break;
     }
     if (SC_TSLEEP) __builtin_amdgcn_s_sleep(SC_TSLEEP);
   }
-  STAMP(1)
   __builtin_amdgcn_s_setprio(3);
   const uint32_t tok_a = lds_addr(&S.ins), tok_v = k + 1;
   uint32_t r[kScG];
@@ -500,13 +402,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       "ds_mskor_rtn_b32 %13, %29, %33, %47\n"
       "ds_mskor_rtn_b32 %14, %30, %32, %48\n"
       "ds_mskor_rtn_b32 %15, %31, %33, %49\n"
-#if SC_DUP & 1
-      "s_waitcnt lgkmcnt(0)\n"
-      "ds_mskor_b32 %16, %32, %34\nds_mskor_b32 %17, %33, %35\nds_mskor_b32 %18, %32, %36\nds_mskor_b32 %19, %33, %37\n"
-      "ds_mskor_b32 %20, %32, %38\nds_mskor_b32 %21, %33, %39\nds_mskor_b32 %22, %32, %40\nds_mskor_b32 %23, %33, %41\n"
-      "ds_mskor_b32 %24, %32, %42\nds_mskor_b32 %25, %33, %43\nds_mskor_b32 %26, %32, %44\nds_mskor_b32 %27, %33, %45\n"
-      "ds_mskor_b32 %28, %32, %46\nds_mskor_b32 %29, %33, %47\nds_mskor_b32 %30, %32, %48\nds_mskor_b32 %31, %33, %49\n"
-#endif
       "ds_write_b32 %50, %51\n"
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
@@ -518,7 +413,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
         "v"(tok_a), "v"(tok_v)
       : "memory");
   __builtin_amdgcn_s_setprio(0);
-  STAMP(2)
 
   // ---- C. one candidate per position: the latest earlier position of the same hash (own slot or
   // the other's, the more recent first) whose first 4 bytes equal the position's.  Only its offset
@@ -546,7 +440,7 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       const uint32_t q = sc0 + 64 * g + lane;
       const uint32_t sh = 16 * (g & 1);
       const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // positions
-      const uint32_t c1 = (SC_ABL & 8) ? q : max(ca, cb), c2 = (SC_ABL & 8) ? q : min(ca, cb);
+      const uint32_t c1 = max(ca, cb), c2 = min(ca, cb);
       const bool ok1 = c1 < q;
       const uint32_t d1 = q - c1, d2 = q - c2;  // the offsets
       uint16_t* const Og = reinterpret_cast<uint16_t*>(Ob8 + (Orel ^ (4u * (g & 7))) + 128u * g);
@@ -574,22 +468,12 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
 #pragma unroll
       for (int j = 0; j < SC_CB; ++j) {
         const int g = g0 + j;
-        const uint32_t q = sc0 + 64 * g + lane;
         const uint32_t sh = 16 * (g & 1);
         const uint32_t ca = (r[g] >> sh) & 0xffffu, cb = (r[g] >> (16 - sh)) & 0xffffu;  // positions
-        c1s[j] = (SC_ABL & 8) ? q : max(ca, cb);
-        c2s[j] = (SC_ABL & 8) ? q : min(ca, cb);
-        if (SC_GC & 1) {
-          v1s[j] = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)c1s[j], 0, 0);
-          v2s[j] = __builtin_amdgcn_raw_buffer_load_b32(gb, (int)c2s[j], 0, 0);
-        } else {
-          v1s[j] = sc_ld32u(S.blk, c1s[j]);
-          v2s[j] = sc_ld32u(S.blk, c2s[j]);
-        }
-        if (SC_DUP & 2) {
-          sc_dup2(lds_addr(S.blk + (c1s[j] & ~3u)));
-          sc_dup2(lds_addr(S.blk + (c2s[j] & ~3u)));
-        }
+        c1s[j] = max(ca, cb);
+        c2s[j] = min(ca, cb);
+        v1s[j] = sc_ld32u(S.blk, c1s[j]);
+        v2s[j] = sc_ld32u(S.blk, c2s[j]);
       }
 #pragma unroll
       for (int j = 0; j < SC_CB; ++j) asm("" : "+v"(v1s[j]), "+v"(v2s[j]));  // (keeps the loads unconditional)
@@ -624,7 +508,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   SC_WL(8) SC_WL(9) SC_WL(10) SC_WL(11) SC_WL(12) SC_WL(13) SC_WL(14) SC_WL(15)
 #undef SC_WL
   __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  STAMP(3)
 
   // ---- D. lane-serial walks over the row, resynchronised ----
   // A lane walks its row greedily: at a match position it computes the match length (16-byte
@@ -671,12 +554,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       } else {
         const uint32_t q = c0 + i, off = offAt(i);
         const uint32_t p = q - off;
-        if (SC_DUP & 4) sc_dup5(lds_addr(S.blk + (q & ~3u)));
-        if (SC_DUP & 8) sc_dup5(lds_addr(S.blk + (p & ~3u)));
-        if (SC_DUP & 16) {
-          uint32_t x;
-          asm volatile("ds_read_u16 %0, %1\ns_waitcnt lgkmcnt(0)" : "=v"(x) : "v"(lds_addr(&Orow[i ^ osw2])) : "memory");
-        }
         // the match length over 16 bytes: the first 4 are equal (the candidate check, C), so bytes
         // [4, 16) of both sides decide it: 4 + the equal leading bytes of 12, or kScExt (17) when
         // all 12 are equal (the min's cap 104 >> 3 = 13); then capped at the super-chunk end
@@ -716,12 +593,11 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     walk(std::false_type{}, row ? 0u : 16u, 0u, P, mp, e);
     if (!row) e = c0;
   }
-  for (; !(SC_ABL & 2);) {
+  for (;;) {
     const uint32_t pe = __builtin_amdgcn_update_dpp(0u, e, 0x138, 0xf, 0xf, false);  // wave_shr:1
     const uint32_t sn = lane == 0 ? sc0 : pe;
     const bool chg = sn != s;
     if (!ballot(chg)) break;
-    STAMP_COUNT(10, 1)
     const bool inrow = chg && sn < ce;  // (an entry is never before the row)
     uint32_t nP, mp, ne;
     walk(std::true_type{}, inrow ? sn - c0 : 16u, P, nP, mp, ne);  // (rows not walking: stop at once)
@@ -755,7 +631,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
       tk.t[j] = off | (L << 16) | (i << 24);
     }
   }
-  STAMP(4)
 
   // ---- E. the lane's summary, literal runs across lanes, sizes, offsets ----
   // lead: the first literal run; trail: the last one when the row ends on literals (no copies:
@@ -798,17 +673,15 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     size = (lead ? (cont ? lead : 1u + lead) : 0u) + body + (trail ? mts + trail : 0u);
   const uint32_t incl = scan_dpp(size);
   const uint32_t total = readlane(incl, 63);
-  STAMP(5)
 
   // ---- F. a staging slot: super-chunk k takes slot k % kScRing once the writer has written
   // super-chunk k - kScRing out of it ----
   const uint32_t slot = k % kScRing;
   (void)sc_wait(&S.rseq[slot], [&](uint32_t v) { return v == k; }, S.err, 2u);
-  STAMP(6)
 
   // ---- G. the lanes' tokens into the slot, then the slot to the writer ----
   uint8_t* const stg = S.ring[slot];
-  if (!(SC_ABL & 1)) {
+  {
     // the output bytes are or-ed into a zeroed slot: no masks, no branches per piece (the zeroes
     // land first: a wave's LDS operations execute in order)
     for (uint32_t u = lane; 16 * u < total; u += 64) reinterpret_cast<uint4*>(stg)[u] = make_uint4(0, 0, 0, 0);
@@ -867,8 +740,6 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
   }
   // (a wave's LDS operations execute in order: the writer that sees the size sees the bytes)
   __hip_atomic_store(&S.rsize[slot], total + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);  // (all lanes: same value)
-  STAMP(7)
-  STAMP_FLUSH(g_stamp_sc)
 }
 
 // the staged bytes [0, len) of an LDS buffer (16-byte aligned) to global g (any alignment): aligned
@@ -905,22 +776,18 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, uint32
                                                                uint32_t k0, uint32_t k1, bool whole,
                                                                uint32_t* len_out, uint32_t lane) {
   uint32_t o = hv, err = 0;
-  STAMP_DECL
   // (the next slot's size word is read together with this slot's bytes: when the workers are ahead,
   // as they mostly are, the next link starts without a poll round trip of its own)
   uint32_t vpre = 0;
   for (uint32_t k = k0; k < k1; ++k) {
     const uint32_t slot = k % kScRing;
     const uint32_t sz =
-        (SC_WPRE && vpre ? vpre : sc_wait(&S.rsize[slot], [](uint32_t v) { return v != 0; }, err, 4u)) - 1;
-    STAMP(8)
+        (vpre ? vpre : sc_wait(&S.rsize[slot], [](uint32_t v) { return v != 0; }, err, 4u)) - 1;
     if (err) break;
-    if (SC_WPRE)
-      vpre = k + 1 < k1 ? uniform(__hip_atomic_load(&S.rsize[(k + 1) % kScRing], __ATOMIC_ACQUIRE,
+    vpre = k + 1 < k1 ? uniform(__hip_atomic_load(&S.rsize[(k + 1) % kScRing], __ATOMIC_ACQUIRE,
                                                     __HIP_MEMORY_SCOPE_WORKGROUP))
                         : 0u;
-    if (!(SC_ABL & 32)) sc_copy_out(dst + o, S.ring[slot], sz, lane);
-    STAMP(9)
+    sc_copy_out(dst + o, S.ring[slot], sz, lane);
     o += sz;
     // (this wave's slot reads are issued before these writes, and LDS runs them in order)
     __hip_atomic_store(&S.rsize[slot], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -951,7 +818,6 @@ __device__ __attribute__((always_inline)) inline void sc_writer(ScLds& S, uint32
   }
   err |= uniform(__hip_atomic_load(&S.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
   if (lane == 0) *len_out = err ? 0xfff00000u | err : o;  // (an error mark: > any block's length)
-  STAMP_FLUSH(g_stamp_sc)
 }
 
 // Persistent: one workgroup per CU walks blocks blockIdx.x, + gridDim.x, ...; each wave loads its
@@ -1031,7 +897,6 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
     __syncthreads();
 
     const uint32_t nsc = (n + kScS - 1) / kScS;
-    const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, (int)n, 0x00020000);
     if (wave == kScWorkers) {
       __builtin_amdgcn_s_setprio(SC_WPRIO);  // (the writer's chain gates the slots)
       sc_writer(S, n, dst, hv, 0, nsc, true, &a.out_len[b], lane);
@@ -1043,7 +908,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
         // every lane adds 1 (one ds_add of 64 after the atomic optimizer); lane 0 sees a multiple of 64
         const uint32_t k = uniform(__hip_atomic_fetch_add(&S.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 6;
         if (k >= nsc) break;
-        sc_superchunk<kDense>(S, k, n, wave, lane, gb);
+        sc_superchunk<kDense>(S, k, n, wave, lane);
       }
     }
     SC_FETCH(bn)  // the next block's bytes, in flight behind the other waves' last super-chunks
@@ -1064,11 +929,6 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc(CompressArgs a) {
 // concatenation of the block's output in k_compress_sc (sans its literal fallback, which the
 // gather checks per block).  Item outputs at out + out_off[block] + j pitch, lengths in
 // part_len[i]; a block the screen emitted as a literal has that literal as its part 0.
-// Diagnostic builds only (-DSC_SPAN_ABL=bits; invalid output, timing only): 1 no table rebuild,
-// 2 no parse (and no writer), 4 no block staging.
-#ifndef SC_SPAN_ABL
-#define SC_SPAN_ABL 0
-#endif
 template <int kDense>
 __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a, ScSpan sp) {
   __shared__ __attribute__((aligned(16))) ScLds S;
@@ -1093,8 +953,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
   const uint8_t* const src = a.in + a.in_off[b];
   uint8_t* const dst = a.out + a.out_off[b] + (uint64_t)j * sp.pitch;
   // ---- stage the block, clear the table (as k_compress_sc) ----
-  if (SC_SPAN_ABL & 4) {
-  } else if (((uintptr_t)src & 15) == 0) {
+  if (((uintptr_t)src & 15) == 0) {
     const uint4* s16 = reinterpret_cast<const uint4*>(src);
     uint4* d16 = reinterpret_cast<uint4*>(S.blk);
     const uint32_t n16 = n >> 4;
@@ -1125,7 +984,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
   // ---- the table as the in-order insert of positions [0, kScS k0) leaves it (section B's values:
   // positions, group parity = slot; positions without 4 bytes before the block end never enter;
   // a never-written slot and position 0 both read 0, the same candidate)
-  const uint32_t pe = (SC_SPAN_ABL & 1) ? 0u : kScS * k0;
+  const uint32_t pe = kScS * k0;
   // (a lane takes four consecutive positions of one group -- two aligned dwords give their four
   // words -- and a wave four groups of the phase's parity per step)
   const uint32_t sub = lane & 15, gq = lane >> 4;
@@ -1157,10 +1016,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
     }
     __syncthreads();
   }
-  const __amdgpu_buffer_rsrc_t gb = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(src), (short)0, (int)n, 0x00020000);
-  if (SC_SPAN_ABL & 2) {
-    if (tid == 0) *plen = 0;
-  } else if (wave == kScWorkers) {
+  if (wave == kScWorkers) {
     __builtin_amdgcn_s_setprio(SC_WPRIO);
     sc_writer(S, n, dst, hv, k0, k1, false, plen, lane);
     __builtin_amdgcn_s_setprio(0);
@@ -1168,7 +1024,7 @@ __global__ __launch_bounds__(kScThreads) void k_compress_sc_span(CompressArgs a,
     for (;;) {
       const uint32_t k = uniform(__hip_atomic_fetch_add(&S.next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 6;
       if (k >= k1) break;
-      sc_superchunk<kDense>(S, k, n, wave, lane, gb);
+      sc_superchunk<kDense>(S, k, n, wave, lane);
     }
   }
 }
@@ -1186,16 +1042,6 @@ hipError_t launch_compress_sc_span(const CompressArgs& a, int mode, const ScSpan
   return hipGetLastError();
 }
 
-#if SM_STAMP
-extern "C" int sm_debug_stamps_sc(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp_sc), sizeof(g_stamp_sc)) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[12] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp_sc), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif
 
 // mode 1 (SM_MODE_FAST): the more recent 4-byte match per position; mode 2 (SM_MODE_FAST_DENSE): the
 // longer of the two candidates over 16 bytes (smaller output, about 15% slower)

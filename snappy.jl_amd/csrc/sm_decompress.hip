@@ -26,28 +26,11 @@
 #include "sm_device.h"
 #include "sm_internal.h"
 
-#ifndef SM_ABLATE_D  // diagnostic builds only: 1 = skip tag execution (walk/decode only), 4 = no HBM sources, 8 = no fence before HBM sources (timing only)
-#define SM_ABLATE_D 0
-#endif
 
-#ifndef SM_DUP_D  // diagnostic builds only: sections run twice (1 walk, 2 decode, 4 flush, 8 execution round) for their instruction counts
-#define SM_DUP_D 0
-#endif
 
-#ifndef SM_DEC_QUEUE  // diagnostic builds only: 1 = persistent waves on a global stream queue (k_decompress_q), 2 = also check the grab
-#define SM_DEC_QUEUE 0
-#endif
-
-#ifndef SM_IDX_NOLANES
-#define SM_IDX_NOLANES 0
-#endif
 
 namespace sm {
 
-#if SM_STAMP
-__device__ unsigned long long g_stamp[10];
-#endif
-STAMP_MACROS(10)
 
 typedef uint16_t __attribute__((aligned(1))) du16u;
 typedef uint32_t __attribute__((aligned(1))) du32u;
@@ -321,12 +304,10 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
   const bool in_al = (((uintptr_t)in) & 3) == 0;
   const int64_t Nm1 = min((int64_t)N - 1, (int64_t)ip_end);  // parse limit
 
-  STAMP_DECL
   // every batch consumes input (ip strictly increases): more than N batches means the wave is
   // not whole (a caller that split it) -- a status, never a hang
   uint32_t guard = N + 1;
   while ((int64_t)ip < Nm1 && op < op_lim) {
-    STAMP_COUNT(6, 1)
     if (__builtin_expect(--guard == 0, 0)) return kErrDevice;
     if (ip >= wb + 256) {
       if (__builtin_expect(ip < wb + 512, 1)) {
@@ -340,19 +321,10 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         issue_pre2 = false;
       }
     }
-    STAMP(0)
     // the window [ip, ip+256) (inside the ring: ip < wb+256; a batch's literals end before
     // ip+256+200 < wb+768)
     const uint32_t wlim = (int64_t)(ip + 256) < Nm1 ? ip + 256 : (uint32_t)Nm1;
     uint32_t cpos, csz, sizes;
-#if SM_DUP_D & 1
-    {  // (diagnostic) the walk once more, its results dropped: its instruction count
-      uint32_t c2, s2, z2, i2 = ip;
-      asm volatile("" : "+v"(i2));
-      const uint32_t n2 = walk_window(ring_get8(ring, i2 + 4 * lane), wlim - ip, jt, lane, c2, s2, z2);
-      asm volatile("" : : "v"(c2), "v"(s2), "v"(z2), "s"(n2) : "memory");
-    }
-#endif
     const uint32_t ntok = walk_window(ring_get8(ring, ip + 4 * lane), wlim - ip, jt, lane, cpos, csz, sizes);
     uint32_t tpos = 0, ipw = ip, tnext = 0;
     bool big = false;
@@ -366,7 +338,6 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       big = ((readlane(sizes, rel >> 2) >> ((rel & 3) * 8)) & 0xff) == 255;
     }
 
-    STAMP(1)
     if (__builtin_expect(ntok != 0, 1)) {
       const bool mine = lane < ntok;
       // one tag per lane: its fields, output offset (wave scan) and the reference's checks as
@@ -408,14 +379,6 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         return d;
       };
       const TagDec d = tag_decode(tpos);
-#if SM_DUP_D & 2
-      {  // (diagnostic) the decode once more, its results dropped: its instruction count
-        uint32_t tp = tpos;
-        asm volatile("" : "+v"(tp));
-        const TagDec e = tag_decode(tp);
-        asm volatile("" : : "v"(e.err), "v"(e.incl), "v"(e.lsrc), "v"(e.offset), "v"(e.litlen));
-      }
-#endif
       const uint32_t len = d.len, offset = d.offset, litlen = d.litlen, incl = d.incl, opt = d.opt, lsrc = d.lsrc;
       const bool iscopy = d.iscopy;
       const int32_t err = d.err;
@@ -430,7 +393,6 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         big = false;  // the next tag is a batch tag inside the window
       }
       const uint32_t X = readlane(incl, nt - 1);
-      STAMP(2)
 
       if (op - wbase + X + 32 > kWin) win_shift(win, wbase, op, lane);  // (uniform)
       const uint32_t O0 = op;
@@ -445,11 +407,11 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const uint64_t all = nt == 64 ? ~0ull : ((1ull << nt) - 1);
       const uint64_t copym = ballot(iscopy) & all;
       const uint64_t longm = ballot(litlen > 64) & ~copym & all;
-      const uint64_t gm = (SM_ABLATE_D & 4) ? 0ull : ballot(slo < wbase) & copym;
+      const uint64_t gm = ballot(slo < wbase) & copym;
       const bool gsrc = inverse_ballot(gm);
       uint64_t done = longm | ~all;
       // HBM sources: this wave's earlier flushes (and big literals) must have landed
-      if (!(SM_ABLATE_D & 8) && gm) __threadfence_block();
+      if (gm) __threadfence_block();
 
       // long literals (65..200 B, no dependencies, inside the input ring): whole-wave passes
       uint64_t lm = longm;
@@ -461,7 +423,6 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         if (k < L) lds_or16(winA + (o - wbase) + k, 0, trim16(lds_get16(ringA + ((sr + k) & (kRing - 1)), 0), min(16u, L - k)));
       }
 
-      STAMP(3)
       // One round (all in LDS, or HBM for sources before the window) runs every tag whose source
       // is final before the batch and whose bytes can be read straight: a literal (<= 64 B, from
       // the input ring) or a copy with offset >= 16 -- output byte j is S[j mod offset]
@@ -469,18 +430,12 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       // output byte j - offset = out[slo + j], written by an earlier 16-byte pass.  So every tag
       // reads out[slo + j] (or its literal bytes) in 16-byte pieces.  The writes never touch
       // bytes another ready tag reads.
-      if (SM_ABLATE_D & 1) done = ~0ull;
       if (__builtin_expect(done != ~0ull, 1)) {
-        STAMP_COUNT(7, 1)
-        const uint64_t rm = ~done & ((SM_ABLATE_D & 2) ? ~0ull : ~copym | (ballot(shi <= O0) & ballot(offset >= 16)));
+        const uint64_t rm = ~done & (~copym | (ballot(shi <= O0) & ballot(offset >= 16)));
         const uint32_t L = iscopy ? len : litlen;
         const uint32_t sa = iscopy ? winA + (slo - wbase) : ringA + (lsrc & (kRing - 1));
         const uint32_t da = winA + (opt - wbase);
         const uint8_t* gs = out + slo;
-#if SM_DUP_D & 8
-        for (int dup = 0; dup < 2; ++dup) {  // (diagnostic) the round twice: or-ing the same bytes again changes nothing
-          asm volatile("" : : : "memory");
-#endif
 #pragma unroll
         for (uint32_t base = 0; base < 64; base += 16) {
           const uint64_t am = rm & ballot(L > base);
@@ -497,13 +452,8 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
             lds_or16(da, base, trim16(v, min(L - base, 16u)));
           }
         }
-#if SM_DUP_D & 8
-        }
-#endif
         done |= rm;
       }
-      STAMP(8)
-      STAMP_COUNT(9, __builtin_popcountll(~done))
       // The copies left -- their source overlaps earlier tags of this batch, or offset < 16 --
       // run in stream order, one tag at a time, a byte per lane: byte k = S[k mod offset] with S
       // final by then (LDS accesses of a wave are serviced in order).
@@ -512,7 +462,6 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       while (rest) {
         const uint32_t t = ctz64(rest);
         rest &= rest - 1;
-        STAMP_COUNT(7, 1)
         const uint32_t o = readlane(opt, t), sl = readlane(slo, t), L = readlane(len, t), off = readlane(offset, t);
         if (lane < L) {
           uint32_t k = lane;
@@ -524,14 +473,9 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
       }
-      STAMP(4)
       op += X;
       if (__builtin_expect(op > op_lim, 0)) return kErrCross;  // a tag crosses the fragment end
       win_flush(out, win, wbase, flushed, op & ~15u, lane);  // whole 16-byte blocks to HBM
-#if SM_DUP_D & 4
-      asm volatile("" : : : "memory");
-      win_flush(out, win, wbase, flushed, op & ~15u, lane);  // (diagnostic) the same bytes again
-#endif
       flushed = max(flushed, op & ~15u);
       ip = ipw;
     }
@@ -618,8 +562,6 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
     }
   }
   win_flush(out, win, wbase, flushed, op, lane);
-  STAMP(5)
-  STAMP_FLUSH(g_stamp)
   op_end = op;
   return kOk;
 }
@@ -690,33 +632,6 @@ __global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a)
   __shared__ __attribute__((aligned(16))) uint8_t swin[kWinPad + kWin];  // output window
   decompress_block(a, blockIdx.x, sring, sjt, swin + kWinPad, lane_id());
 }
-
-#if SM_DEC_QUEUE
-// Diagnostic variant: persistent waves taking streams from a global
-// counter.  The grab is lane 0's atomic add made wave-uniform by v_readfirstlane -- the round-4
-// variant's hang came from a grab that was not: decode_stream_batch needs the whole wave (its
-// walk reads other lanes through ds_bpermute, and an inactive lane reads 0), so a wave split by
-// a per-lane grab computes no tags, makes no progress and loops.  Bounded twice: at most nblk + 1
-// grabs per wave, and decode_stream_batch gives up with kErrDevice after N batches.  The host
-// zeroes the counter before each launch (sm_api.hip).
-__device__ unsigned int g_dec_queue;
-__global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress_q(DecompressArgs a) {
-  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + kRingMirror];
-  __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];
-  __shared__ __attribute__((aligned(16))) uint8_t swin[kWinPad + kWin];
-  const uint32_t lane = lane_id();
-  for (uint32_t it = 0; it <= a.nblk; ++it) {
-    uint32_t b = 0;
-    if (lane == 0) b = atomicAdd(&g_dec_queue, 1u);
-    b = uniform(b);
-#if SM_DEC_QUEUE > 1
-    if (__builtin_amdgcn_readlane(b, 63) != b) printf("k_decompress_q: wave grab not uniform (%u)\n", b);
-#endif
-    if (b >= a.nblk) break;
-    decompress_block(a, b, sring, sjt, swin + kWinPad, lane);
-  }
-}
-#endif
 
 // ---- one large stream, decoded in parallel ------------------------
 // Snappy.jl (src/Snappy.jl:29-33), libsnappy and this library compress 64 KiB blocks
@@ -957,7 +872,7 @@ __global__ __launch_bounds__(index_threads(kDeep)) void k_stream_index(const uin
     const uint64_t rl = lim > s ? lim - s : 0;  // chunk-relative parse limit
     uint64_t x = lane, ex = exit0;
     uint32_t pre = 0, res = tot0;
-    bool done = lane == 0 || SM_IDX_NOLANES;  // (SM_IDX_NOLANES: timing variant only)
+    bool done = lane == 0;
     uint16_t* tj = jt;                                   // 2 x 256 u16
     uint32_t* to = reinterpret_cast<uint32_t*>(jt + 512);  // 2 x 256 u32 (jt holds 3 KiB here)
     while (true) {
@@ -1388,6 +1303,16 @@ constexpr uint32_t kRunDone = 0xffffffffu;
 #define SM_CHAIN_DEEPLINK 1  // links through chain 0's deep records (0: entry records only)
 #endif
 static_assert((1u << kLift) >= kChainNodes, "the jump tables must reach every node");
+// k_stream_chain's static LDS, summed against the 160 KiB a workgroup may declare (ADVICE round 5:
+// at kC = 1024 the kernel uses ~159 KiB, so growing kChainPool, kChainPath, kLift, kIdxPad or
+// OriginPath by a little fails here, where these constants are tuned, not in the compiler)
+template <uint32_t kC>
+constexpr uint32_t chain_lds_bytes() {
+  return 4 * kChainPool + (uint32_t)sizeof(OriginPath) * kChainPath + 2 * kLift * kChainNodes +
+         (5 * 4 + 1) * kChainNodes + 4 * 5 + 2 * kJt + (kC + kIdxPad + 16) + 64 /* alignment slack */;
+}
+static_assert(chain_lds_bytes<1024>() <= 160u * 1024 && chain_lds_bytes<512>() <= 160u * 1024,
+              "k_stream_chain's LDS arrays exceed 160 KiB");
 // an entry record (exit, output) of chunk base `base`, compact: (output << 16) | (exit - base)
 __device__ inline uint32_t rec_compact(uint2 r, uint64_t base) {
   const uint64_t d = (uint64_t)r.x - base;
@@ -1887,28 +1812,8 @@ hipError_t launch_decompress_frags(const uint8_t* in, uint32_t N, uint32_t size,
 
 hipError_t launch_decompress(const DecompressArgs& a, int /*large*/, hipStream_t s) {
   if (a.nblk == 0) return hipSuccess;
-#if SM_DEC_QUEUE
-  if (!a.one_n) {  // (diagnostic build) one wave per resident slot: 256 CUs x 4 SIMDs x SM_DEC_OCC
-    const unsigned int zero = 0;
-    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_dec_queue), &zero, sizeof(zero), 0, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_decompress_q, dim3(min(a.nblk, 256u * 4u * SM_DEC_OCC)), dim3(64), 0, s, a);
-    return hipGetLastError();
-  }
-#endif
   hipLaunchKernelGGL(k_decompress, dim3(a.nblk), dim3(64), 0, s, a);
   return hipGetLastError();
 }
-
-#if SM_STAMP
-extern "C" int sm_debug_stamps(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamp), sizeof(g_stamp)) != hipSuccess) return -1;
-  if (reset) {
-    unsigned long long z[10] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_stamp), z, sizeof(z)) != hipSuccess) return -1;
-  }
-  return 0;
-}
-#endif
 
 }  // namespace sm

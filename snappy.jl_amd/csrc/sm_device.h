@@ -8,47 +8,6 @@
 
 namespace sm {
 
-// Diagnostic builds only (-DSM_STAMP=1, tools/stamp_run.py): per-wave s_memtime section
-// stamps, summed into a device array by lane 0 when a wave finishes.
-#ifndef SM_STAMP
-#define SM_STAMP 0
-#endif
-#if SM_STAMP
-#define STAMP_MACROS(NS) constexpr int kStampSlots = NS;
-// (s_memtime in volatile asm with a memory clobber: the builtin can be moved across the code it
-// is meant to bracket)
-__device__ inline uint64_t stamp_now() {
-  uint64_t t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : : "memory");
-  return t;
-}
-#define STAMP_DECL                   \
-  uint64_t st_acc[kStampSlots] = {}; \
-  uint64_t st_t = stamp_now();
-#define STAMP(i)                     \
-  {                                  \
-    const uint64_t t_ = stamp_now(); \
-    st_acc[i] += t_ - st_t;          \
-    st_t = t_;                       \
-  }
-#define STAMP_COUNT(i, v) st_acc[i] += (v);
-#define STAMP_FLUSH(arr) \
-  if (lane == 0)         \
-    for (int i_ = 0; i_ < kStampSlots; ++i_) atomicAdd(&arr[i_], (unsigned long long)st_acc[i_]);
-#elif defined(SM_MARKS)  // static listing only (-DSM_MARKS -S): section marks in the assembly
-#define STAMP_MACROS(NS)
-#define STAMP_DECL
-#define STAMP(i) asm volatile("; SCMARK " #i);
-#define STAMP_COUNT(i, v)
-#define STAMP_FLUSH(arr)
-#else
-#define STAMP_MACROS(NS)
-#define STAMP_DECL
-#define STAMP(i)
-#define STAMP_COUNT(i, v)
-#define STAMP_FLUSH(arr)
-#endif
-
 constexpr uint32_t kBlockSize = 65536;        // internal.jl:31
 constexpr uint32_t kInputMarginBytes = 15;    // internal.jl:32
 constexpr uint32_t kMaxHashTableSize = 16384; // internal.jl:33

@@ -137,6 +137,10 @@ hipError_t launch_parts_gather(const uint8_t* src, const uint64_t* out_off, cons
                                uint8_t* dst, hipStream_t s);
 hipError_t launch_frag_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* out_len,
                               const uint32_t* in_len, uint32_t nfrag, uint64_t* tot, uint8_t* dst, hipStream_t s);
+// a sharded stream's fragments at their global offsets (sm_place_fragments_device, k_place)
+hipError_t launch_place(const uint8_t* src, const uint64_t* src_off, const uint32_t* len, const uint64_t* dst_off,
+                        uint32_t nfrag, uint64_t total, int header, uint64_t cap, uint8_t* dst, uint64_t* loc_off,
+                        int32_t* status, hipStream_t s);
 // concatenate per-fragment outputs into one stream after a varint header (single-buffer API)
 hipError_t launch_gather(const uint8_t* src, const uint64_t* src_off, const uint32_t* len,
                          const uint64_t* dst_off, uint8_t* dst, uint32_t nblk, hipStream_t s);

@@ -11,8 +11,11 @@ block-relative), so the path shards with no data-path collective:
 * one large stream (config 5): fragments [lo, hi) of the stream go to each rank; each rank
   compresses its fragments (no per-fragment header, table size from the TOTAL length, Q2);
   one all-gather of the u32 fragment sizes gives every rank the global exclusive scan, i.e.
-  where its fragments land after the varint(total) header.  That all-gather is the only
-  collective on the path (10,304 fragments x 4 B for 644 MiB).
+  where its fragments land after the varint(total) header (`stream_offsets_device`).  That
+  all-gather is the only collective on the path (10,304 fragments x 4 B for 644 MiB).  Each
+  rank then writes its fragments at those offsets into its byte range of the stream with
+  sm_place_fragments_device (rank 0: the varint header first); the ranges are contiguous, so
+  a D2H of each range at its offset (or a gather of the ranges) is the stream.
 
 The per-rank compressor is injected (`compress_fn`) so that the CPU tests can run the
 distributed logic with gloo, using the oracle as a stand-in for the GPU kernels.
@@ -82,7 +85,8 @@ def compress_stream_sharded(data, rank, world, compress_fn, group=None):
 
     compress_fn(list_of_fragments, total_len) -> list of compressed fragments (no headers).
     Returns (header, local_fragments, global_offsets_of_local_fragments, total_compressed_len);
-    header + all ranks' fragments written at their offsets is the snappy stream of `data`."""
+    header + all ranks' fragments written at their offsets is the snappy stream of `data` (on the
+    device: sm_place_fragments_device writes them there, place_fragments_device in the package)."""
     import torch
     total = len(data)
     offs, lens = fragment_bounds(total)
@@ -94,15 +98,6 @@ def compress_stream_sharded(data, rank, world, compress_fn, group=None):
     header = varint32(total)
     starts = len(header) + np.concatenate([[0], np.cumsum(sizes)[:-1]]) if len(sizes) else np.zeros(0, np.int64)
     return header, out, starts[lo:hi], int(len(header) + sizes.sum())
-
-
-def assemble(header, pieces_with_offsets, total_len):
-    """Concatenate (offset, bytes) pieces from all ranks behind the header."""
-    buf = bytearray(total_len)
-    buf[: len(header)] = header
-    for off, piece in pieces_with_offsets:
-        buf[int(off): int(off) + len(piece)] = piece
-    return bytes(buf)
 
 
 def stream_offsets_device(local_sizes, total_len, rank, world, group=None):

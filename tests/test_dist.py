@@ -22,6 +22,16 @@ def _free_port():
     return port
 
 
+def _join(header, pieces_with_offsets, total_len):
+    """The checker's concatenation of (offset, bytes) pieces behind the header (the product
+    places them on the device: sm_place_fragments_device, tests/test_dist_gpu.py)."""
+    buf = bytearray(total_len)
+    buf[: len(header)] = header
+    for off, piece in pieces_with_offsets:
+        buf[int(off): int(off) + len(piece)] = piece
+    return bytes(buf)
+
+
 def _worker(rank, world, port, fname, q):
     import torch.distributed as dist
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -43,7 +53,7 @@ def _worker(rank, world, port, fname, q):
         pieces = [None] * world
         dist.all_gather_object(pieces, list(zip(offs.tolist(), local)))
         allp = [p for rp in pieces for p in rp]
-        stream = D.assemble(header, allp, total_c)
+        stream = _join(header, allp, total_c)
         q.put((rank, stream))
     finally:
         dist.destroy_process_group()

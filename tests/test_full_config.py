@@ -10,7 +10,7 @@
   with valid copy-4 tags / offsets >= 65,536 through sm_uncompress (src/internal.jl:19,26-28:
   the decoder must not rely on the absence of long back-references).
 * config 5 as fragments: sm_compress_fragments_device + sm_uncompress_fragments_device over the
-  644 MiB stream; the assembled stream decodes under the oracle.
+  644 MiB stream; the stream placed on the device decodes under the oracle.
 """
 import os
 import sys
@@ -173,8 +173,9 @@ def test_copy4_long_offsets_uncompress(sm, oracle, gpu_available):
 
 def test_config5_fragments_device_roundtrip(sm, oracle, gpu_available):
     """Config 5 through the fragment entry points the sharded bench uses (all fragments on one
-    GPU here): the assembled stream decodes under the oracle; the fragment decoder restores
-    every fragment."""
+    GPU here): the stream placed on the device by sm_place_fragments_device equals the checker's
+    concatenation of the fragment slots behind the header and decodes under the oracle; the
+    fragment decoder restores every fragment from the placed stream."""
     import torch
     bench = _bench()
     big = bench.large_corpus()
@@ -182,13 +183,20 @@ def test_config5_fragments_device_roundtrip(sm, oracle, gpu_available):
     sh.compress(sm)
     from importlib import import_module
     D = import_module("snappy_jl_amd.dist")
+    sh.index(D, 0, 1)
+    sh.place(sm)
+    torch.cuda.synchronize()
+    assert int(sh.place_status.item()) == 0
+    placed = sh.d_stream[: sh.range_bytes()].cpu().numpy().tobytes()
+    assert len(placed) == int(sh.stream_len.item())
     hl = D.varint32(big.size)
     lens = sh.comp_len.cpu().numpy().astype(np.int64)
     comp = sh.d_comp.cpu().numpy()
     stream = bytearray(hl)
     for f, n in enumerate(lens):
         stream += comp[f * SLOT: f * SLOT + n].tobytes()
-    assert oracle.uncompress(bytes(stream)) == big.tobytes()
+    assert placed == bytes(stream)
+    assert oracle.uncompress(placed) == big.tobytes()
     sh.d_dec.fill_(0)
     sh.uncompress(sm)
     torch.cuda.synchronize()

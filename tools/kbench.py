@@ -59,6 +59,8 @@ def fragments(sm, dev, args):
     nfrag = (big.size + bench.BLOCK - 1) // bench.BLOCK
     sh = bench.StreamShard(big, 0, nfrag, dev)
     sh.compress(sm)
+    sh.index(bench.load_dist(), 0, 1)  # (world 1, no process group: the scan alone)
+    sh.place(sm)  # (the fragments decode from the placed stream)
     torch.cuda.synchronize()
     fn = (lambda: sh.compress(sm)) if args.op == "compress_fragments" else (lambda: sh.uncompress(sm))
     fn()
@@ -69,7 +71,6 @@ def fragments(sm, dev, args):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.reps
     print("%s: %.3f ms/launch, %.2f GB/s (uncompressed bytes)" % (args.op, dt * 1e3, sh.in_bytes / dt / 1e9))
-    sh.index(bench.load_dist(), 0, 1)  # (world 1, no process group: the scan alone)
     print("roundtrip ok:", sh.verify(sm))
 
 
