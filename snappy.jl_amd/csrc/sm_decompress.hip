@@ -500,6 +500,24 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const int64_t avail_in = (int64_t)N - (int64_t)lsrc;
       if (avail_out < (int64_t)litlen || avail_in < (int64_t)litlen) return kErrLiteral;  // :518
       if ((uint64_t)op + litlen > op_lim) return kErrCross;
+      if (litlen <= kMaxBatchLit) {
+        // a short literal with 2-4 length bytes (a non-minimal encoding, or a wrapped length): its
+        // bytes are in the ring (the tag is in the batch window, ip < wb + 512, so lsrc + litlen <
+        // wb + 717 < wb + 768), so the whole wave ors them into the window as the batch round does
+        // its long literals, then flushes whole 16-byte blocks as a batch does -- no full flush and
+        // window reload from HBM per such tag.  (Every byte before op & ~15 is in
+        // HBM here, as after a batch: a shift drops only flushed bytes.)
+        if (op - wbase + litlen + 32 > kWin) win_shift(win, wbase, op, lane);  // (uniform)
+        const uint32_t k = 16 * lane;
+        if (k < litlen)
+          lds_or16(winA + (op - wbase) + k, 0, trim16(lds_get16(ringA + ((lsrc + k) & (kRing - 1)), 0), min(16u, litlen - k)));
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        op += litlen;
+        win_flush(out, win, wbase, flushed, op & ~15u, lane);
+        flushed = max(flushed, op & ~15u);
+        ip = lsrc + litlen;
+        continue;
+      }
       win_flush(out, win, wbase, flushed, op, lane);  // HBM holds everything before the literal
       // bulk copy: head bytes to 16-B source alignment, then 16 B per lane, 4 in flight
       const uint8_t* s = in + lsrc;

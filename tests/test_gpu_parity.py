@@ -271,6 +271,71 @@ def test_fast_mode_largest_superchunk_outputs(sm, oracle, gpu_available, mode):
         assert len(out) <= 3 + 3 + len(blk)
 
 
+def superchunk_sizes(stream, sc=1024):
+    """Output bytes per 1 KiB input super-chunk of a fast-mode stream: every tag (with its literal
+    bytes) counted in the super-chunk where its input starts.  In k_compress_sc's streams no tag
+    crosses a super-chunk end (copies stop there, literal runs are not merged across it), so these
+    are the sizes the super-chunks had in their staging slots."""
+    pos, ip = 0, 0
+    while stream[ip] & 0x80:
+        ip += 1
+    ip += 1
+    sizes = {}
+    while ip < len(stream):
+        c, start, tip = stream[ip], pos, ip
+        kind = c & 3
+        if kind == 0:
+            n = c >> 2
+            if n < 60:
+                ip += 1
+                n += 1
+            else:
+                k = n - 59
+                n = int.from_bytes(stream[ip + 1: ip + 1 + k], "little") + 1
+                ip += 1 + k
+            ip += n
+            pos += n
+        else:
+            ip += {1: 2, 2: 3, 3: 5}[kind]
+            pos += 4 + ((c >> 2) & 7) if kind == 1 else (c >> 2) + 1
+        s = start // sc
+        assert (pos - 1) // sc == s, "a tag crosses a super-chunk end"
+        sizes[s] = sizes.get(s, 0) + ip - tip
+    return sizes
+
+
+@pytest.mark.parametrize("mode", FAST_MODES)
+def test_fast_mode_superchunk_bound_reached(sm, oracle, gpu_available, mode):
+    """The staging slot's bound, reached: one super-chunk of each block is 61-64-byte
+    literal runs (2-byte tags) between 4-byte copies from more than 2 KiB back (3-byte tags), the
+    rest of the block a repeat, so the block keeps its parse (no whole-block literal fallback)
+    and its stream shows every super-chunk's staged size.  The largest reaches the analytic bound
+    of 1,040 bytes to within a few bytes and stays within kScSlot - 24 = 1,064."""
+    rng = np.random.default_rng(0x5108)
+    base = rng.integers(0, 256, 4096, dtype=np.uint8).tobytes()
+    blocks = []
+    for run in (61, 62, 63, 64):
+        for phase in (0, 5, 31, 60):
+            worst = [rng.integers(0, 256, phase, dtype=np.uint8).tobytes()]
+            n = phase
+            while n < 2048 + 128:
+                src = int(rng.integers(0, 2048 - 8))
+                worst += [rng.integers(0, 256, run, dtype=np.uint8).tobytes(), base[src:src + 4]]
+                n += run + 4
+            head = base + b"".join(worst)[:2048]  # the worst pattern over super-chunks 4 and 5
+            blocks.append(head + base[:4096] * ((65536 - len(head)) // 4096 + 1))
+    blocks = [b[:65536] for b in blocks]
+    outs = sm.compress_batch(blocks, mode=mode)
+    best = 0
+    for blk, out in zip(blocks, outs):
+        assert oracle.uncompress(out) == blk
+        assert len(out) < len(blk) // 2  # the parse was kept
+        sz = superchunk_sizes(out)
+        assert max(sz.values()) <= 1040
+        best = max(best, sz.get(4, 0), sz.get(5, 0))
+    assert best >= 1030, best
+
+
 # ---- decompress -------------------------------------------------------------------------
 
 def test_decompress_corpus_and_golden(sm, oracle, libsnappy, gpu_available, corpus):
@@ -491,6 +556,39 @@ def test_decompress_nonminimal_literals(sm, oracle, gpu_available):
         assert oracle.uncompress(s) == expect
     for s, expect in built[:40]:
         assert sm.validate(s) == 0
+        assert sm.uncompress(s) == expect
+
+
+def test_decompress_consecutive_nonminimal_literals(sm, oracle, gpu_available):
+    """Long runs of consecutive short literals with 2-4 length bytes (each one a tag the batch walk
+    stops at, decoded into the LDS window without a batch between them: many window shifts
+    with no batch flush in between), then copies from anywhere before (window and HBM sources,
+    offsets up to 65,535)."""
+    from streams import copy_tag, varint
+    rng = np.random.default_rng(0x6161)
+    streams = []
+    for _ in range(40):
+        body, out = bytearray(), bytearray()
+        target = int(rng.integers(3000, 65536))
+        while len(out) < target:
+            for _ in range(int(rng.integers(1, 80))):
+                n = int(rng.integers(1, 201))
+                k = int(rng.integers(2, 5))
+                data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+                body += bytes([(59 + k) << 2]) + (n - 1).to_bytes(k, "little") + data
+                out += data
+            for _ in range(int(rng.integers(1, 4))):
+                off = int(rng.integers(1, min(len(out), 65535) + 1))
+                ln = int(rng.integers(4, 65))
+                body += copy_tag(off, ln)
+                for _ in range(ln):
+                    out.append(out[-off])
+        streams.append((varint(len(out)) + bytes(body), bytes(out)))
+    outs = _decode_all(sm, [s for s, _ in streams])
+    for (s, expect), o in zip(streams, outs):
+        assert o == expect
+        assert oracle.uncompress(s) == expect
+    for s, expect in streams[:8]:
         assert sm.uncompress(s) == expect
 
 

@@ -53,7 +53,10 @@ def main():
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
-    blocks = bench.text_blocks(a.blocks, 0x5EED) if a.data == "text" else bench.random_blocks(a.blocks, 0x5EED + 1)
+    if a.data == "large":  # config 5's corpus cut into its 10,304 64 KiB fragments, as a batch of blocks
+        blocks = bench.large_corpus().reshape(-1, bench.BLOCK)
+    else:
+        blocks = bench.text_blocks(a.blocks, 0x5EED) if a.data == "text" else bench.random_blocks(a.blocks, 0x5EED + 1)
     B = bench.Batch(blocks, dev)
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     libs = [(os.path.basename(x), *load(x)) for x in a.libs]

@@ -1,13 +1,7 @@
-# A/B timing of library variants (design tool; run on the GPU box): tools/gpu_ab.sh <tag> lib...
-# the in-tree library first, then each variant, twice in alternation; kbench checks the round trip
+# A/B of library builds in tools/ablib on the GPU box: bash tools/gpu_ab.sh <tag> "<ab_raw args>" lib1 lib2 ...
 set -u
 O=gpurun_out/$1; shift
+ARGS=$1; shift
 mkdir -p $O
-for rep in 1 2; do
-  for L in default "$@"; do
-    if [ "$L" = default ]; then unset SNAPPY_MI355X_LIB; else export SNAPPY_MI355X_LIB=$L; fi
-    timeout -k 10 120 python3 tools/kbench.py --op ${OP:-compress_fast} --blocks 10000 --reps 20 > $O/k.log 2>&1 || { echo "$L failed"; tail $O/k.log; exit 1; }
-    echo "$L: $(grep -v amdgpu.ids $O/k.log | tr '\n' ' ')"
-  done
-done
-unset SNAPPY_MI355X_LIB
+timeout -k 10 400 python3 tools/ab_raw.py $ARGS "$@" > $O/ab.log 2>&1 || { echo ab failed; tail -20 $O/ab.log; exit 1; }
+grep -v amdgpu.ids $O/ab.log | tail -25
