@@ -92,6 +92,8 @@ struct sm_ctx {
   std::vector<hipEvent_t> ev;     // their completion events
   DevBuf in, out, out2, meta, idx, gat, org;  // org: origin pointers of the general parallel decode
   HostBuf stage;
+  HostBuf stage_in;              // small host inputs on their way up (upload_input)
+  hipEvent_t in_ev = nullptr;    // recorded behind the last upload from stage_in
   int last_path = -1;  // sm_ctx_last_path
   bool small = true;   // sm_ctx_set_small_decode
   bool split = true;   // sm_ctx_set_split_compress
@@ -149,6 +151,38 @@ constexpr uint32_t kPieceFrags = 256;        // 16 MiB per piece
 #define SM_OUT_PIECE 2048
 #endif
 constexpr uint32_t kOutPieceFrags = SM_OUT_PIECE;  // sm_uncompress: output pieces (128 MiB)
+
+constexpr size_t kPinnedInMin = 32u << 10;  // host inputs from this size up go through stage_in
+constexpr size_t kPinnedInMax = 16u << 20;  // ... up to this size
+
+// A host input of a single-buffer call into ctx->in.  Inputs of 32 KiB to 16 MiB are copied on
+// the host into the context's pinned, device-mapped staging and moved to the device by a copy
+// kernel (k_to_host reading the mapped pages): fireworks.jpeg's uncompress 60 -> 50 us, html's
+// 70 -> 67, 64 KiB compress 52 -> 48 (profiles/r06_upload_ab.txt).  Smaller inputs stay with the
+// runtime's pageable copy, which is 2-4 us faster there than the staging (its event and the
+// extra launch), and so does an upload through the copy engine from the staging at every size.
+// The staging is reused by the next call only after the previous upload's event.
+hipError_t upload_input(sm_ctx* ctx, const void* src, size_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (n >= kPinnedInMin && n <= kPinnedInMax && ctx->stage_in.ensure(n + 16) == hipSuccess && ctx->stage_in.dp) {
+    if (!ctx->in_ev) {
+      const hipError_t e = hipEventCreateWithFlags(&ctx->in_ev, hipEventDisableTiming);
+      if (e != hipSuccess) {
+        ctx->in_ev = nullptr;
+        return e;
+      }
+    } else {
+      const hipError_t e = hipEventSynchronize(ctx->in_ev);
+      if (e != hipSuccess) return e;
+    }
+    memcpy(ctx->stage_in.p, src, n);
+    const hipError_t e = sm::launch_to_host((const uint8_t*)ctx->stage_in.dp, (uint32_t)n, (uint8_t*)ctx->in.p,
+                                            nullptr, 0, nullptr, s);
+    if (e != hipSuccess) return e;
+    return hipEventRecord(ctx->in_ev, s);
+  }
+  return hipMemcpyAsync(ctx->in.p, src, n, hipMemcpyHostToDevice, s);
+}
 
 // the context's copy stream and at least n events (created on first use)
 hipError_t ensure_copy_stream(sm_ctx* ctx, size_t n) {
@@ -667,6 +701,8 @@ void sm_ctx_destroy(sm_ctx* ctx) {
     ctx->gat.release();
     ctx->org.release();
     ctx->stage.release();
+    ctx->stage_in.release();
+    if (ctx->in_ev) (void)hipEventDestroy(ctx->in_ev);
     if (ctx->copy) {
       (void)hipStreamSynchronize(ctx->copy);
       (void)hipStreamDestroy(ctx->copy);
@@ -885,7 +921,7 @@ sm_status sm_validate_compressed_buffer(sm_ctx* ctx, const char* compressed, siz
   const uint64_t zero = 0;
   const uint32_t len32 = (uint32_t)n;
   int32_t st = SM_ERR_DEVICE;
-  if (n) SM_CHECK(hipMemcpyAsync(ctx->in.p, compressed, n, hipMemcpyHostToDevice, s));
+  SM_CHECK(upload_input(ctx, compressed, n, s));
   SM_CHECK(hipMemcpyAsync(d_off, &zero, 8, hipMemcpyHostToDevice, s));
   SM_CHECK(hipMemcpyAsync(d_len, &len32, 4, hipMemcpyHostToDevice, s));
   SM_CHECK(sm::launch_validate((const uint8_t*)ctx->in.p, d_off, d_len, 1, d_status, s));
@@ -952,7 +988,7 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
     const uint32_t span = (uint32_t)((SM_BLOCK_SIZE / 1024 + parts - 1) / parts);
     const size_t sl = parts > 1 ? std::max<size_t>(slot, (size_t)parts * span * sm::kSpanSlot) : slot;
     SM_CHECK(ctx->out.ensure((size_t)nfrag * sl));
-    SM_CHECK(hipMemcpyAsync(ctx->in.p, input, n, hipMemcpyHostToDevice, s));
+    SM_CHECK(upload_input(ctx, input, n, s));
     sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
                        nfrag, sm::hashtable_size(n), 0};
     if (mode == SM_MODE_REFERENCE) {
@@ -1055,7 +1091,7 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   int32_t* d_status = (int32_t*)(m + 20);
   uint32_t hv[2] = {(uint32_t)n, size};
   HT_DECL
-  SM_CHECK(hipMemcpyAsync(ctx->in.p, compressed, n, hipMemcpyHostToDevice, s));
+  SM_CHECK(upload_input(ctx, compressed, n, s));
   HT("uncompress: H2D input")
   // a large stream: fragments in parallel when it is block-structured (Snappy.jl, libsnappy
   // and this library all write such streams); otherwise, or on any error, the in-order decode

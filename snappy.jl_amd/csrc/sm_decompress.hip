@@ -285,6 +285,10 @@ __device__ inline uint32_t walk_window(uint64_t cw, uint32_t rlim, uint16_t* jt1
 // refused with kErrCross: a fragment of a block-structured stream must not read output that
 // other waves produce (the caller then decodes the whole stream in order instead).  Error
 // checks use stream-global positions, so they are the reference's whatever the range.
+// kLit: 16-byte loads per lane in flight in a long literal's bulk copy (4 in the batch kernels,
+// whose VGPR budget sets their occupancy; 16 in the lone-stream kernel, where one wave's copy is
+// latency-bound)
+template <uint32_t kLit = 4>
 __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t N, uint32_t ip, uint32_t ip_end,
                                        uint32_t size, uint8_t* out, uint32_t op0, uint32_t frag_lo, uint8_t* ring,
                                        uint16_t* jt, uint8_t* win, uint32_t lane, uint32_t& op_end,
@@ -519,7 +523,7 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
         continue;
       }
       win_flush(out, win, wbase, flushed, op, lane);  // HBM holds everything before the literal
-      // bulk copy: head bytes to 16-B source alignment, then 16 B per lane, 4 in flight
+      // bulk copy: head bytes to 16-B source alignment, then 16 B per lane, kLit in flight
       const uint8_t* s = in + lsrc;
       uint32_t head = (uint32_t)((16 - ((uintptr_t)s & 15)) & 15);
       if (head > litlen) head = litlen;
@@ -528,16 +532,15 @@ __device__ int32_t decode_stream_batch(const uint8_t* __restrict__ in, uint32_t 
       const uint32_t n16 = (litlen - head) >> 4;
       uint8_t* d = out + op + head;
       uint32_t k = lane;
-      for (; k + 3 * kWave < n16; k += 4 * kWave) {
-        uint4 v0 = s16[k], v1 = s16[k + kWave], v2 = s16[k + 2 * kWave], v3 = s16[k + 3 * kWave];
-        *reinterpret_cast<du64u*>(d + 16 * k) = ((uint64_t)v0.y << 32) | v0.x;
-        *reinterpret_cast<du64u*>(d + 16 * k + 8) = ((uint64_t)v0.w << 32) | v0.z;
-        *reinterpret_cast<du64u*>(d + 16 * (k + kWave)) = ((uint64_t)v1.y << 32) | v1.x;
-        *reinterpret_cast<du64u*>(d + 16 * (k + kWave) + 8) = ((uint64_t)v1.w << 32) | v1.z;
-        *reinterpret_cast<du64u*>(d + 16 * (k + 2 * kWave)) = ((uint64_t)v2.y << 32) | v2.x;
-        *reinterpret_cast<du64u*>(d + 16 * (k + 2 * kWave) + 8) = ((uint64_t)v2.w << 32) | v2.z;
-        *reinterpret_cast<du64u*>(d + 16 * (k + 3 * kWave)) = ((uint64_t)v3.y << 32) | v3.x;
-        *reinterpret_cast<du64u*>(d + 16 * (k + 3 * kWave) + 8) = ((uint64_t)v3.w << 32) | v3.z;
+      for (; k + (kLit - 1) * kWave < n16; k += kLit * kWave) {
+        uint4 v[kLit];
+#pragma unroll
+        for (uint32_t j = 0; j < kLit; ++j) v[j] = s16[k + j * kWave];
+#pragma unroll
+        for (uint32_t j = 0; j < kLit; ++j) {
+          *reinterpret_cast<du64u*>(d + 16 * (k + j * kWave)) = ((uint64_t)v[j].y << 32) | v[j].x;
+          *reinterpret_cast<du64u*>(d + 16 * (k + j * kWave) + 8) = ((uint64_t)v[j].w << 32) | v[j].z;
+        }
       }
       for (; k < n16; k += kWave) {
         uint4 v0 = s16[k];
@@ -616,6 +619,7 @@ __device__ inline int32_t parse_header(const uint8_t* in, uint32_t N, uint32_t l
 #define SM_DEC_OCC 7  // waves per SIMD: 67 VGPRs, 5.0 KB LDS per wave (8: 64 VGPRs with a spill, 1.444 against 1.357 ms)
 #endif
 // one stream of the batch (block b) by one wave
+template <uint32_t kLit = 4>
 __device__ inline void decompress_block(const DecompressArgs& a, uint32_t b, uint8_t* sring, uint16_t* sjt, uint8_t* swin,
                                         uint32_t lane) {
   const uint8_t* in = a.one_n ? a.in : a.in + a.in_off[b];
@@ -635,7 +639,7 @@ __device__ inline void decompress_block(const DecompressArgs& a, uint32_t b, uin
   if (st == kOk && size > cap) st = kBufferTooSmall;
   if (st == kOk) {
     uint32_t op_end = 0;
-    st = decode_stream_batch(in, N, ip, N, size, dst, 0, 0, sring, sjt, swin, lane, op_end);
+    st = decode_stream_batch<kLit>(in, N, ip, N, size, dst, 0, 0, sring, sjt, swin, lane, op_end);
     if (st == kOk && op_end != size) st = kErrInvalid;                                    // Snappy.jl:50
   }
   if (lane == 0) {
@@ -649,6 +653,17 @@ __global__ __launch_bounds__(64, SM_DEC_OCC) void k_decompress(DecompressArgs a)
   __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];  // tag-walk jump tables
   __shared__ __attribute__((aligned(16))) uint8_t swin[kWinPad + kWin];  // output window
   decompress_block(a, blockIdx.x, sring, sjt, swin + kWinPad, lane_id());
+}
+
+// sm_uncompress's in-order path (a.one_n: one stream, one wave): the same engine with 16 loads a
+// lane in flight in long literals -- a lone wave's bulk copy is bound by load latency, not by the
+// VGPRs that set the batch kernel's occupancy (fireworks.jpeg's literal-only stream: see
+// DESIGN.md section 3.4)
+__global__ __launch_bounds__(64, 1) void k_decompress_one(DecompressArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t sring[kRing + kRingMirror];
+  __shared__ __attribute__((aligned(16))) uint16_t sjt[kJt];
+  __shared__ __attribute__((aligned(16))) uint8_t swin[kWinPad + kWin];
+  decompress_block<16>(a, 0, sring, sjt, swin + kWinPad, lane_id());
 }
 
 // ---- one large stream, decoded in parallel ------------------------
@@ -1735,7 +1750,8 @@ __global__ __launch_bounds__(256) void k_origin_gather(const uint8_t* __restrict
     out[x] = in[P[x] & 0x7fffffffu];
 }
 
-// src[0, n) -> dst and nw control words -> words (dst / words: pinned host memory, device-mapped),
+// src[0, n) -> dst and nw control words -> words (dst / words: pinned host memory, device-mapped;
+// sm_api.hip's upload_input runs it the other way, from mapped host pages into device memory),
 // 16 bytes a thread; src and dst 16-byte aligned.
 __global__ __launch_bounds__(256) void k_to_host(const uint8_t* __restrict__ src, uint32_t n, uint8_t* __restrict__ dst,
                                                  const uint32_t* wsrc, uint32_t nw, uint32_t* words) {
@@ -1830,7 +1846,10 @@ hipError_t launch_decompress_frags(const uint8_t* in, uint32_t N, uint32_t size,
 
 hipError_t launch_decompress(const DecompressArgs& a, int /*large*/, hipStream_t s) {
   if (a.nblk == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_decompress, dim3(a.nblk), dim3(64), 0, s, a);
+  if (a.one_n && a.nblk == 1)
+    hipLaunchKernelGGL(k_decompress_one, dim3(1), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_decompress, dim3(a.nblk), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 

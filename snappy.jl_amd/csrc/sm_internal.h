@@ -106,7 +106,8 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
                                uint32_t nchunks, uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P,
                                uint32_t rounds, uint8_t* out, uint32_t* words, hipStream_t s);
 // src[0, n) to dst and wsrc[0, nw) to words by a kernel (dst, words: device-mapped pinned host
-// memory; no copy engine behind the kernels).  src, dst 16-byte aligned; nw <= 256.
+// memory; no copy engine behind the kernels -- or, for uploads, src mapped host memory and dst
+// the device's).  src, dst 16-byte aligned; nw <= 256.
 hipError_t launch_to_host(const uint8_t* src, uint32_t n, uint8_t* dst, const uint32_t* wsrc, uint32_t nw,
                           uint32_t* words, hipStream_t s);
 hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s);
