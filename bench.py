@@ -49,7 +49,7 @@ BLOCK = 65536
 SLOT = 76496  # >= max_compressed_length(65536) = 76490, 16-B aligned
 HBM_PEAK_GBPS = 8000.0
 METRIC = "GB/s compressed+decompressed (batched blocks) at 1/2/4/8 GPUs; % HBM peak"  # BASELINE.json
-ROUND = "r05"
+ROUND = "r06"
 
 # test/runtests.jl:8-24, the round-trip corpus; config 5 tiles it
 ROUNDTRIP_FILES = ["alice29.txt", "asyoulik.txt", "html", "html_x_4", "kppkn.gtb", "lcet10.txt", "fireworks.jpeg",

@@ -1,7 +1,7 @@
 """Kernel driver for profiling (rocprofv3 --kernel-trace / --pmc): runs one codec kernel R
 times on the bench workload (text or random 64 KiB blocks), device-resident.
 
-  python tools/kbench.py --op compress_fast|compress_ref|uncompress --blocks 2000 --reps 5 [--data random]
+  python tools/kbench.py --op compress_fast|compress_ref|uncompress|uncompress_reference --blocks 2000 --reps 5 [--data random]
 """
 import argparse
 import os
@@ -29,13 +29,15 @@ def main():
         return fragments(sm, dev, args)
     blocks = bench.text_blocks(args.blocks, 0x5EED) if args.data == "text" else bench.random_blocks(args.blocks, 0x5EED + 1)
     b = bench.Batch(blocks, dev)
-    b.compress(sm, "fast")
+    # uncompress_reference: the decode of the reference-mode (Snappy.jl byte-identical) streams
+    b.compress(sm, "reference" if args.op == "uncompress_reference" else "fast")
     torch.cuda.synchronize()
     ops = {
         "compress_fast": lambda: b.compress(sm, "fast"),
         "compress_dense": lambda: b.compress(sm, "dense"),
         "compress_ref": lambda: b.compress(sm, "reference"),
         "uncompress": lambda: b.uncompress(sm),
+        "uncompress_reference": lambda: b.uncompress(sm),
     }
     fn = ops[args.op]
     fn()
@@ -48,7 +50,7 @@ def main():
     nbytes = args.blocks * bench.BLOCK
     print("%s %s: %.3f ms/launch, %.2f GB/s (uncompressed bytes), ratio %.4f" % (
         args.op, args.data, dt * 1e3, nbytes / dt / 1e9, float(b.comp_len.sum()) / nbytes))
-    if args.op != "uncompress":
+    if not args.op.startswith("uncompress"):
         b.uncompress(sm)
     print("roundtrip ok:", b.verify())
 

@@ -24,7 +24,8 @@ KERNELS = {"compress_fast": ("pmc_compress", ["k_literal_screen", "k_compress_sc
            "uncompress": ("pmc_uncompress", ["k_decompress("]),
            "compress_fast_random": ("pmc_compress_random", ["k_literal_screen", "k_compress_sc<0>"]),
            "uncompress_random": ("pmc_uncompress_random", ["k_decompress("]),
-           "compress_fragments": ("pmc_compress_fragments", ["k_literal_screen", "k_compress_sc<0>"])}
+           "compress_fragments": ("pmc_compress_fragments", ["k_literal_screen", "k_compress_sc<0>"]),
+           "uncompress_reference_streams": ("pmc_uncompress_reference", ["k_decompress("])}
 IN_BYTES = 10000 * 65536  # uncompressed bytes per launch (tools/pmc_run.sh BLOCKS=10000)
 IN_BYTES_FRAG = 675282944  # config 5's stream (bench.CONFIG5_BYTES)
 
