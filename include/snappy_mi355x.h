@@ -86,10 +86,12 @@ void* sm_ctx_stream(sm_ctx* ctx);
  * 1 as parallel 64 KiB fragments (a large block-structured stream), 2 in parallel by origin
  * pointers (a large stream whose copies cross 64 KiB blocks), 3 a large stream's first error
  * found in parallel (per-tag checks over its tag path), 4 a small stream (<= 1 MiB compressed)
- * decoded in parallel by origin pointers entirely on the device (one synchronisation), -1 none yet */
+ * decoded in parallel by origin pointers entirely on the device (one synchronisation), 5 a stream
+ * of literal tags only (at most 16, e.g. an incompressible input's) copied by one kernel from the
+ * pinned input staging to the pinned output staging (one synchronisation), -1 none yet */
 int sm_ctx_last_path(sm_ctx* ctx);
-/* diagnostic: enable (1, the default) or disable (0) path 4 for the ctx's sm_uncompress calls
- * (the tests run the other paths on small streams with it off) */
+/* diagnostic: enable (1, the default) or disable (0) paths 4 and 5 for the ctx's sm_uncompress
+ * calls (the tests run the other paths on small streams with them off) */
 sm_status sm_ctx_set_small_decode(sm_ctx* ctx, int enable);
 /* diagnostic: enable (1, the default) or disable (0) parsing the fragments of a small fast-mode
  * sm_compress input (<= 4 MiB) in parts on their own workgroups -- the same bytes as the

@@ -184,6 +184,65 @@ hipError_t upload_input(sm_ctx* ctx, const void* src, size_t n, hipStream_t s) {
   return hipMemcpyAsync(ctx->in.p, src, n, hipMemcpyHostToDevice, s);
 }
 
+// sm_uncompress path 5: are the stream's tags literals only?  At most kLitSpans of them (an
+// incompressible input's stream has one literal per 64 KiB block), each with at most 3 length
+// bytes, inside the input and the declared length, together covering both exactly.  Then the
+// reference's decode (internal.jl:411-527: every tag starts before the input's last byte, and
+// copy_literal!'s checks pass) is those literals' bytes in order, and Snappy.jl:50's length check
+// holds.  Anything else -- a copy tag, a 4-byte length, more tags, a stream that ends early or
+// late -- is not path 5, and the other paths reproduce the reference's accept/reject.  Reads the
+// tag headers only (at most 4 bytes a tag); the bytes move on the device.
+bool literal_only(const uint8_t* c, size_t n, size_t hdr, uint32_t size, sm::LitSpans& sp) {
+  size_t p = hdr;
+  uint64_t o = 0;
+  sp.n = 0;
+  while (p < n) {
+    if (sp.n == sm::kLitSpans) return false;
+    const uint32_t t = c[p];
+    if (t & 3) return false;  // a copy
+    uint64_t len = (t >> 2) + 1;
+    size_t q = p + 1;
+    if ((t >> 2) >= 60) {
+      const uint32_t nb = (t >> 2) - 59;
+      if (nb > 3 || q + nb > n) return false;
+      uint32_t v = 0;
+      for (uint32_t k = 0; k < nb; ++k) v |= (uint32_t)c[q + k] << (8 * k);
+      len = (uint64_t)v + 1;
+      q += nb;
+    }
+    if (q + len > n || o + len > size) return false;
+    sp.src[sp.n] = (uint32_t)q;
+    sp.dst[sp.n] = (uint32_t)o;
+    ++sp.n;
+    o += len;
+    p = q + len;
+  }
+  sp.dst[sp.n] = (uint32_t)o;
+  return sp.n > 0 && o == size;
+}
+
+// path 5: the input into the pinned staging on the host, the literals to the pinned output by
+// k_literal_spans reading and writing the mapped pages, then the bytes to the caller.  1: done,
+// 0: not taken (no mapped staging), -1: a device error.
+int literal_uncompress(sm_ctx* ctx, const uint8_t* comp, size_t n, uint32_t size, const sm::LitSpans& ls,
+                       uint8_t* host_out) {
+  hipStream_t s = ctx->stream;
+  const size_t w_off = align_up(size, 256);
+  if (ctx->stage_in.ensure(n + 16) != hipSuccess || !ctx->stage_in.dp) return 0;
+  if (ctx->stage.ensure(w_off + 64) != hipSuccess || !ctx->stage.dp) return 0;
+  if (ctx->in_ev && hipEventSynchronize(ctx->in_ev) != hipSuccess) return -1;  // (a previous upload's reads)
+  memcpy(ctx->stage_in.p, comp, n);
+  uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
+  volatile uint32_t* const w = (volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off);
+  w[1] = 0xffffffffu;  // (the kernel writes SM_OK)
+  if (sm::launch_literal_spans((const uint8_t*)ctx->stage_in.dp, ls, sdp, (uint32_t*)(sdp + w_off), s) != hipSuccess)
+    return -1;
+  if (hipStreamSynchronize(s) != hipSuccess) return -1;
+  if (w[1] != 0 || w[0] != size) return -1;
+  memcpy(host_out, ctx->stage.p, size);
+  return 1;
+}
+
 // the context's copy stream and at least n events (created on first use)
 hipError_t ensure_copy_stream(sm_ctx* ctx, size_t n) {
   if (!ctx->copy) {
@@ -1091,12 +1150,26 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   int32_t* d_status = (int32_t*)(m + 20);
   uint32_t hv[2] = {(uint32_t)n, size};
   HT_DECL
+  size_t hdr = 0;
+  (void)sm_parse32((const uint8_t*)compressed, n, 0, &size, &hdr);
+  // path 5: literal tags only (an incompressible input) -- one copy kernel from the pinned input
+  // staging to the pinned output staging, one synchronisation
+  {
+    sm::LitSpans ls;
+    if (ctx->small && size <= kPinnedOutMax && n <= kPinnedInMax && literal_only((const uint8_t*)compressed, n, hdr, size, ls)) {
+      const int r = literal_uncompress(ctx, (const uint8_t*)compressed, n, size, ls, (uint8_t*)uncompressed);
+      if (r < 0) return SM_ERR_DEVICE;
+      if (r == 1) {
+        ctx->last_path = 5;
+        *uncompressed_length = size;
+        return SM_OK;
+      }
+    }
+  }
   SM_CHECK(upload_input(ctx, compressed, n, s));
   HT("uncompress: H2D input")
   // a large stream: fragments in parallel when it is block-structured (Snappy.jl, libsnappy
   // and this library all write such streams); otherwise, or on any error, the in-order decode
-  size_t hdr = 0;
-  (void)sm_parse32((const uint8_t*)compressed, n, 0, &size, &hdr);
   // (a body longer than its output is all literals, which the in-order engine copies HBM to HBM at
   // bandwidth: path 0 is faster there -- fireworks.jpeg 59 us against ~100; a body just under
   // its output is random data with short copies sprinkled in, which path 0 walks in small batches

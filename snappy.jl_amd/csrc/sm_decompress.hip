@@ -1763,6 +1763,45 @@ __global__ __launch_bounds__(256) void k_to_host(const uint8_t* __restrict__ src
   if (t < n - 16 * n16) dst[16 * n16 + t] = src[16 * n16 + t];
 }
 
+// path 5 (sm_uncompress): the literals of a literal-only stream to their output positions --
+// copy_literal! (internal.jl:500-527) for every tag at once.  A thread takes 16 output bytes: one
+// literal's bytes as five dword loads and four funnel shifts, one 16-byte store; a unit that
+// straddles two literals or the end goes byte by byte.
+__global__ __launch_bounds__(256) void k_literal_spans(const uint8_t* __restrict__ in, LitSpans sp,
+                                                       uint8_t* __restrict__ out, uint32_t* words) {
+  const uint32_t total = sp.dst[sp.n];
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t == 0) {
+    words[0] = total;
+    words[1] = 0;  // SM_OK
+  }
+  for (uint32_t x = 16 * t; x < total; x += 16 * blockDim.x * gridDim.x) {
+    uint32_t s = 0;
+    for (uint32_t k = 1; k < sp.n; ++k) s = sp.dst[k] <= x ? k : s;
+    if (x + 16 <= sp.dst[s + 1]) {
+      const uint32_t p = sp.src[s] + (x - sp.dst[s]);
+      const uint32_t* w = reinterpret_cast<const uint32_t*>(in + (p & ~3u));
+      const uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+      *reinterpret_cast<uint4*>(out + x) =
+          make_uint4(__builtin_amdgcn_alignbyte(w1, w0, p), __builtin_amdgcn_alignbyte(w2, w1, p),
+                     __builtin_amdgcn_alignbyte(w3, w2, p), __builtin_amdgcn_alignbyte(w4, w3, p));
+    } else {
+      for (uint32_t y = x; y < min(x + 16, total); ++y) {
+        while (s + 1 < sp.n && sp.dst[s + 1] <= y) ++s;
+        out[y] = in[sp.src[s] + (y - sp.dst[s])];
+      }
+    }
+  }
+}
+
+hipError_t launch_literal_spans(const uint8_t* in, const LitSpans& sp, uint8_t* out, uint32_t* words, hipStream_t s) {
+  if (sp.n == 0 || sp.n > kLitSpans) return hipErrorInvalidValue;
+  const uint32_t units = (sp.dst[sp.n] + 15) / 16;
+  const uint32_t grid = min(1024u, max(1u, (units + 255) / 256));
+  hipLaunchKernelGGL(k_literal_spans, dim3(grid), dim3(256), 0, s, in, sp, out, words);
+  return hipGetLastError();
+}
+
 hipError_t launch_to_host(const uint8_t* src, uint32_t n, uint8_t* dst, const uint32_t* wsrc, uint32_t nw,
                           uint32_t* words, hipStream_t s) {
   if (nw > 256) return hipErrorInvalidValue;

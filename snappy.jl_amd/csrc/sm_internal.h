@@ -110,6 +110,17 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
 // the device's).  src, dst 16-byte aligned; nw <= 256.
 hipError_t launch_to_host(const uint8_t* src, uint32_t n, uint8_t* dst, const uint32_t* wsrc, uint32_t nw,
                           uint32_t* words, hipStream_t s);
+// sm_uncompress path 5: a stream of at most kLitSpans literal tags.  Literal s's bytes are at
+// in + src[s] (any alignment) and go to out + dst[s], dst[s + 1] = dst[s] + its length, dst[n] the
+// stream's length (the declared one, which the literals cover exactly); words[0..1] = (length,
+// SM_OK) behind the bytes.  in and out may be device-mapped host memory.
+constexpr uint32_t kLitSpans = 16;
+struct LitSpans {
+  uint32_t src[kLitSpans];
+  uint32_t dst[kLitSpans + 1];
+  uint32_t n;
+};
+hipError_t launch_literal_spans(const uint8_t* in, const LitSpans& sp, uint8_t* out, uint32_t* words, hipStream_t s);
 hipError_t launch_origin_gather(const uint8_t* in, const uint32_t* P, uint32_t size, uint8_t* out, hipStream_t s);
 // sm_compress, small inputs (at most 64 fragments), without host round trips: the fragments'
 // offsets and lengths (fragment f = input [64 KiB f, +64 KiB), output slot f at pitch `slot`);

@@ -609,6 +609,101 @@ def small_path(sm, comp):
             and body <= size)
 
 
+def literal_path(sm, comp, limit=16):
+    """Whether sm_uncompress takes path 5 (sm_api.hip literal_only): at most `limit` literal tags
+    with at most 3 length bytes, covering the body and the declared length exactly."""
+    size, p = sm.parse32(comp, 0)
+    o = n = 0
+    while p < len(comp):
+        t = comp[p]
+        if t & 3 or n == limit:
+            return False
+        ln, q = (t >> 2) + 1, p + 1
+        if (t >> 2) >= 60:
+            nb = (t >> 2) - 59
+            if nb > 3 or q + nb > len(comp):
+                return False
+            ln, q = int.from_bytes(comp[q:q + nb], "little") + 1, q + nb
+        if q + ln > len(comp) or o + ln > size:
+            return False
+        o, p, n = o + ln, q + ln, n + 1
+    return n > 0 and o == size
+
+
+def expected_small(sm, comp):
+    """The single-call path of a stream with paths 4-5 on: 5, 4 or None (another path)."""
+    if literal_path(sm, comp) and sm.parse32(comp, 0)[0] <= (16 << 20):
+        return 5
+    return 4 if small_path(sm, comp) else None
+
+
+def _lit_stream(size, pieces, nb=None):
+    """A stream of literal tags over `pieces` (bytes each), declared length `size`; nb forces the
+    number of length bytes (a non-minimal encoding when the length would fit fewer)."""
+    out = bytearray(bytes(encode32_py(size)))
+    for b in pieces:
+        v = len(b) - 1
+        k = nb if nb is not None else (0 if v < 60 else 1 if v < 256 else 2 if v < 65536 else 3)
+        out.append(v << 2 if k == 0 else (59 + k) << 2)
+        out += v.to_bytes(k, "little") if k else b""
+        out += b
+    return bytes(out)
+
+
+def encode32_py(v):
+    out = bytearray()
+    while v >= 0x80:
+        out.append((v & 0x7f) | 0x80)
+        v >>= 7
+    out.append(v)
+    return out
+
+
+def test_uncompress_literal_only_streams(sm, oracle, libsnappy, gpu_available):
+    """Path 5 (sm_api.hip literal_only + k_literal_spans): streams of at most 16 literal tags --
+    incompressible inputs from every compressor, and hand-built ones with non-minimal length
+    encodings -- decode bit-exactly in one copy kernel; everything that is not exactly such a
+    stream (17 tags, a 4-byte length, a declared length the literals miss, a truncated or
+    over-long body, a copy tag) takes the other paths with the oracle's status."""
+    rng = np.random.default_rng(0x11)
+    for n in (1, 15, 16, 17, 100, 4096, 65535, 65536, 65537, 123093, 1_000_000):
+        data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        for comp in (sm.compress(data, mode="fast"), oracle.compress(data), libsnappy.compress(data)):
+            assert literal_path(sm, comp), n
+            assert sm.uncompress(comp) == data
+            assert sm.last_uncompress_path() == 5
+    data = rng.integers(0, 256, 70_000, dtype=np.uint8).tobytes()
+    cuts = [0, 1, 61, 300, 4000, 20_000, 65_000, 70_000]
+    pieces = [data[a:b] for a, b in zip(cuts, cuts[1:])]
+    for nb in (None, 3):  # (nb 3: every literal with three length bytes)
+        comp = _lit_stream(len(data), pieces, nb)
+        assert oracle.uncompress(comp) == data
+        assert sm.uncompress(comp) == data and sm.last_uncompress_path() == 5
+    many = [data[i * 100:(i + 1) * 100] for i in range(17)]
+    for k, want5 in ((16, True), (17, False)):
+        comp = _lit_stream(100 * k, many[:k])
+        assert sm.uncompress(comp) == data[:100 * k]
+        assert (sm.last_uncompress_path() == 5) == want5
+    # not literal-only, or not exactly covering: the reference's verdict through the other paths
+    four = bytes(encode32_py(300)) + bytes([63 << 2]) + (299).to_bytes(4, "little") + data[:300]  # four length bytes
+    bad = [four,
+           _lit_stream(5000, [data[:4000]]),                # declared length longer than the literals
+           _lit_stream(4000, [data[:4000]])[:-1],           # truncated body
+           _lit_stream(4000, [data[:4000]]) + b"\x00",     # a byte after the last literal
+           _lit_stream(4000, [data[:4000]]) + b"\x01\x02",  # a copy tag after it
+           _lit_stream(3000, [data[:4000]])]                # literals longer than declared
+    for comp in bad:
+        st_o, out_o = oracle.uncompress_status(comp)
+        try:
+            st_g, out_g = 0, sm.uncompress(comp)
+        except sm.SnappyError as exc:
+            st_g, out_g = exc.code, None
+        assert st_g == st_o, (st_g, st_o)
+        if st_o == 0:
+            assert out_g == out_o
+        assert sm.last_uncompress_path() != 5
+
+
 def test_uncompress_large_stream_parallel(sm, oracle, libsnappy, gpu_available):
     """Block-structured streams (Snappy.jl = oracle, libsnappy, this library's fast mode) of
     more than 4 fragments decode through the parallel fragment path, bit-exactly -- or, with a
@@ -626,12 +721,12 @@ def test_uncompress_large_stream_parallel(sm, oracle, libsnappy, gpu_available):
             for data in (raw, noise, mixed, blocky):
                 for comp in (oracle.compress(data), libsnappy.compress(data), sm.compress(data, mode="fast")):
                     assert sm.uncompress(comp) == data
-                    want = 4 if small and small_path(sm, comp) else 1
+                    want = (expected_small(sm, comp) or 1) if small else 1
                     assert sm.last_uncompress_path() == want
                     seen.add(want)
     finally:
         sm.set_small_decode(True)
-    assert seen == {1, 4}
+    assert seen == {1, 4, 5}
 
 
 def test_uncompress_large_stream_fallbacks(sm, oracle, gpu_available):
