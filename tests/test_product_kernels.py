@@ -20,7 +20,7 @@ PRODUCT_KERNELS = {
     "k_gather", "k_gather16", "k_gather_parts", "k_frag_plan", "k_place",
     "k_decompress", "k_decompress_one", "k_decompress_frags", "k_validate", "k_uncompressed_length",
     "k_stream_index", "k_stream_chain", "k_origin_fill", "k_origin_fill_dev", "k_origin_resolve",
-    "k_origin_gather", "k_small_resolve", "k_to_host", "k_path_check",
+    "k_origin_gather", "k_small_resolve", "k_to_host", "k_path_check", "k_literal_spans",
 }
 DIAGNOSTIC = re.compile(r"_q$|queue|stamp|probe|abl|dup|debug", re.I)
 
