@@ -237,19 +237,44 @@ def length_uncompressed(data):
     return parse32(data, 0)
 
 
+_tls = threading.local()
+_SCRATCH_MAX = 64 << 20  # single-call outputs up to this size land in a reused per-thread buffer
+
+
+def _out_buffer(n):
+    """(address, owner) of n writable bytes: the calling thread's reused scratch for outputs up
+    to _SCRATCH_MAX (a single call's fixed cost is a few microseconds, so no allocation and no
+    numpy address lookup per call), else a fresh array."""
+    if n > _SCRATCH_MAX:
+        a = np.empty(max(n, 1), dtype=np.uint8)
+        return a.__array_interface__["data"][0], a
+    buf = getattr(_tls, "buf", None)
+    if buf is None or buf.size < n:
+        buf = np.empty(max(n, 1 << 20), dtype=np.uint8)
+        _tls.buf, _tls.ptr = buf, buf.__array_interface__["data"][0]
+    return _tls.ptr, buf
+
+
+def _in_arg(data):
+    """(pointer argument, length, owner) of an input: bytes go to ctypes as they are (no copy)."""
+    if isinstance(data, bytes):
+        return (data if data else None), len(data), data
+    a = _bytes(data)
+    return (a.__array_interface__["data"][0] if a.size else None), a.size, a
+
+
 def compress(data, mode="fast", device=0):
     """Snappy.jl:20-36 (and the String method :38), computed on the GPU."""
-    src = _bytes(data)
-    if src.size > 0xFFFFFFFF:
+    src, n, keep = _in_arg(data)
+    if n > 0xFFFFFFFF:
         raise SnappyError(16)
-    cap = maxlength_compressed(src.size)
-    out = np.empty(cap, dtype=np.uint8)
+    cap = 32 + n + n // 6  # maxlength_compressed, Snappy.jl:80-82
+    ptr, buf = _out_buffer(cap)
     ol = ctypes.c_size_t(cap)
-    st = lib().sm_compress(context(device), src.ctypes.data if src.size else None, src.size, out.ctypes.data,
-                           ctypes.byref(ol), _mode(mode))
+    st = lib().sm_compress(context(device), src, n, ptr, ctypes.byref(ol), _mode(mode))
     if st:
         raise SnappyError(st)
-    return out[: ol.value].tobytes()
+    return ctypes.string_at(ptr, ol.value)
 
 
 def find_match_length(buf, i1, i2, limit):
@@ -292,17 +317,28 @@ def last_compress_split(device=0):
     return int(lib().sm_ctx_last_compress_split(context(device))) == 1
 
 
+def _declared_length(b):
+    """The varint header's value (src/varint.jl:12-37), only to size the output: 0 when it does
+    not parse (sm_uncompress then returns the reference's header error itself)."""
+    v = 0
+    for i in range(min(5, len(b))):
+        c = b[i]
+        v |= (c & 0x7F) << (7 * i)
+        if c < 0x80:
+            return v if v <= 0xFFFFFFFF else 0
+    return 0
+
+
 def uncompress(data, device=0):
     """Snappy.jl:46-52, computed on the GPU; raises SnappyError with the reference message."""
-    src = _bytes(data)
-    size, _ = length_uncompressed(src)
-    out = np.empty(max(size, 1), dtype=np.uint8)
+    src, n, keep = _in_arg(data)
+    size = _declared_length(keep if isinstance(keep, bytes) else memoryview(keep))
+    ptr, buf = _out_buffer(size)
     ol = ctypes.c_size_t(size)
-    st = lib().sm_uncompress(context(device), src.ctypes.data if src.size else None, src.size, out.ctypes.data,
-                             ctypes.byref(ol))
+    st = lib().sm_uncompress(context(device), src, n, ptr, ctypes.byref(ol))
     if st:
         raise SnappyError(st)
-    return out[: ol.value].tobytes()
+    return ctypes.string_at(ptr, ol.value)
 
 
 # ---- batched host API ---------------------------------------------------------------
