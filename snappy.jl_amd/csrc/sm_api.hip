@@ -494,7 +494,11 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   const uint32_t chunk = small_chunk(n - ip0, size);
   const uint32_t nchunks = (n - ip0 + chunk - 1) / chunk;
   uint32_t rounds = 1;  // kSmallHops^rounds >= size: every chain (at most size steps) resolves
-  for (uint64_t reach = sm::kSmallHops; reach < size; reach *= sm::kSmallHops) ++rounds;
+  uint32_t hops = sm::kSmallHops;
+  if (size <= sm::kOneLaunchHops)
+    hops = std::max(hops, size);  // one launch of size hops (tweet-sized streams: one dispatch fewer)
+  else
+    for (uint64_t reach = sm::kSmallHops; reach < size; reach *= sm::kSmallHops) ++rounds;
   const size_t path_off = align_up((size_t)nchunks * kIdxEntries * 8 + (size_t)nchunks * sm::kDeepChains * sm::kDeepLevels * 16, 256);  // records, deep records
   const size_t ctl_off = align_up(path_off + (size_t)nchunks * sizeof(sm::OriginPath), 256);
   const size_t ctl_n = 4 + rounds;
@@ -512,7 +516,7 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   // the third verdict word is written by the device only when a pointer stays unresolved
   ((volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off))[2] = 0;
   if (sm::launch_small_decode((const uint8_t*)ctx->in.p, n, ip0, size, chunk, nchunks, (uint32_t*)ib,
-                              (sm::OriginPath*)(ib + path_off), d_ctl, (uint32_t*)ctx->org.p, rounds,
+                              (sm::OriginPath*)(ib + path_off), d_ctl, (uint32_t*)ctx->org.p, rounds, hops,
                               pin_out ? sdp : (uint8_t*)ctx->out.p, (uint32_t*)(sdp + w_off), s) != hipSuccess)
     return -1;
   if (!pin_out && hipMemcpyAsync(host_out, ctx->out.p, size, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;

@@ -1677,8 +1677,8 @@ __global__ __launch_bounds__(64) void k_origin_fill_dev(const uint8_t* __restric
   if (st != kOk && lane_id() == 0) atomicOr(&ctl[2], 1u);
 }
 
-// Pointer jumping with up to kHops chain steps per pointer per launch: after launch r every
-// unresolved pointer has moved >= kHops^(r+1) steps, so ceil(log_kHops(size)) launches resolve
+// Pointer jumping with up to `hops` chain steps per pointer per launch: after launch r every
+// unresolved pointer has moved >= hops^(r+1) steps, so ceil(log_hops(size)) launches resolve
 // all.  One pointer per thread (a pointer's hops are one dependent chain, so more threads hide
 // more); a byte is written to out in the launch in which its pointer resolves (the gather folded
 // in: a pointer resolved at the start of launch r > 0 was written before).  Launch r > 0 returns
@@ -1686,9 +1686,10 @@ __global__ __launch_bounds__(64) void k_origin_fill_dev(const uint8_t* __restric
 // after launch r).  Launch 0's first thread publishes
 // the call's verdict words (ctl[1], ctl[2]); nothing else runs when the chain or a fill failed (P
 // is then not all written).  out and words may be device-mapped pinned host memory.
-constexpr uint32_t kHops = kSmallHops;
+// (hops: kSmallHops, or up to kOneLaunchHops for a stream that small -- one launch then resolves
+// every chain, whose length is at most size, without a second launch's dispatch)
 __global__ __launch_bounds__(256) void k_small_resolve(const uint8_t* __restrict__ in, uint32_t* P, uint32_t size,
-                                                       uint32_t* ctl, uint32_t r, uint32_t last,
+                                                       uint32_t* ctl, uint32_t r, uint32_t last, uint32_t hops,
                                                        uint8_t* __restrict__ out, uint32_t* words) {
   uint32_t* const pend = ctl + 4;
   const uint32_t t0 = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1711,9 +1712,9 @@ __global__ __launch_bounds__(256) void k_small_resolve(const uint8_t* __restrict
     // v < x: an earlier byte of the chain.  Every few hops the progress is published, so chains
     // through x jump over it (any value a thread stores or reads is a point of the same chain, so
     // stale or racing values are still correct): a run's chain then shrinks by doubling in
-    // practice, while kHops per launch bounds the work the round count assumes.
+    // practice, while `hops` per launch bounds the work the round count assumes.
 #pragma unroll 1
-    for (uint32_t h = 0; h < kHops && !(v >> 31); ++h) {
+    for (uint32_t h = 0; h < hops && !(v >> 31); ++h) {
       v = P[v];
       if ((h & 3) == 3) P[x] = v;
     }
@@ -1845,8 +1846,9 @@ static void launch_small_front(const uint8_t* in, uint32_t N, uint32_t ip0, uint
 
 hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t chunk,
                                uint32_t nchunks, uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P,
-                               uint32_t rounds, uint8_t* out, uint32_t* words, hipStream_t s) {
-  if (nchunks == 0 || size == 0 || rounds == 0 || 4 + rounds > kWave) return hipErrorInvalidValue;
+                               uint32_t rounds, uint32_t hops, uint8_t* out, uint32_t* words, hipStream_t s) {
+  if (nchunks == 0 || size == 0 || rounds == 0 || 4 + rounds > kWave || hops == 0 || hops > kOneLaunchHops)
+    return hipErrorInvalidValue;
   if (chunk == kSmallChunk)
     launch_small_front<kSmallChunk>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
   else if (chunk == kSmallChunkFine)
@@ -1858,7 +1860,7 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
   const uint32_t g1 = min(32768u, max(1u, (size + 255) / 256));
   for (uint32_t r = 0; r < rounds; ++r)
     hipLaunchKernelGGL(k_small_resolve, dim3(r == 0 ? g1 : min(g1, 32u)), dim3(256), 0, s, in, P, size, ctl, r,
-                       (uint32_t)(r + 1 == rounds), out, words);
+                       (uint32_t)(r + 1 == rounds), hops, out, words);
   return hipGetLastError();
 }
 

@@ -62,6 +62,7 @@ constexpr uint32_t kSmallChunkFine = 512;
 #define SM_SMALL_HOPS 1024
 #endif
 constexpr uint32_t kSmallHops = SM_SMALL_HOPS;  // path 4: chain steps per pointer per resolve launch
+constexpr uint32_t kOneLaunchHops = 65536;       // path 4: outputs up to this size resolve in one launch of size hops
 constexpr uint32_t kDeepLevels = 4;     // path 4: deep-entry records per chain (consecutive long literals)
 constexpr uint32_t kDeepChains = 4;     // path 4: deep-record chains per chunk (distinct entry-lane exits)
 constexpr uint32_t kIdxPad = 288;     // staged bytes past a chunk: +16 entry slack, a 256-byte walk window + 16
@@ -104,7 +105,7 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
 // nonzero word: fall back.  out and words may be device-mapped pinned host memory.
 hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t chunk,
                                uint32_t nchunks, uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P,
-                               uint32_t rounds, uint8_t* out, uint32_t* words, hipStream_t s);
+                               uint32_t rounds, uint32_t hops, uint8_t* out, uint32_t* words, hipStream_t s);
 // src[0, n) to dst and wsrc[0, nw) to words by a kernel (dst, words: device-mapped pinned host
 // memory; no copy engine behind the kernels -- or, for uploads, src mapped host memory and dst
 // the device's).  src, dst 16-byte aligned; nw <= 256.
