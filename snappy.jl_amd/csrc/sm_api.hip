@@ -496,7 +496,7 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   uint32_t rounds = 1;  // kSmallHops^rounds >= size: every chain (at most size steps) resolves
   uint32_t hops = sm::kSmallHops;
   if (size <= sm::kOneLaunchHops)
-    hops = std::max(hops, size);  // one launch of size hops (tweet-sized streams: one dispatch fewer)
+    hops = std::max(hops, size);  // one launch of size hops (up to 256 KiB of output: one dispatch fewer)
   else
     for (uint64_t reach = sm::kSmallHops; reach < size; reach *= sm::kSmallHops) ++rounds;
   const size_t path_off = align_up((size_t)nchunks * kIdxEntries * 8 + (size_t)nchunks * sm::kDeepChains * sm::kDeepLevels * 16, 256);  // records, deep records

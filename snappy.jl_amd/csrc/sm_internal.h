@@ -62,7 +62,7 @@ constexpr uint32_t kSmallChunkFine = 512;
 #define SM_SMALL_HOPS 1024
 #endif
 constexpr uint32_t kSmallHops = SM_SMALL_HOPS;  // path 4: chain steps per pointer per resolve launch
-constexpr uint32_t kOneLaunchHops = 65536;       // path 4: outputs up to this size resolve in one launch of size hops
+constexpr uint32_t kOneLaunchHops = 256u << 10;  // path 4: outputs up to this size resolve in one launch of size hops
 constexpr uint32_t kDeepLevels = 4;     // path 4: deep-entry records per chain (consecutive long literals)
 constexpr uint32_t kDeepChains = 4;     // path 4: deep-record chains per chunk (distinct entry-lane exits)
 constexpr uint32_t kIdxPad = 288;     // staged bytes past a chunk: +16 entry slack, a 256-byte walk window + 16
