@@ -482,9 +482,12 @@ constexpr uint32_t kSmallMaxChunks = (1u << 20) / sm::kSmallChunk;  // compresse
 #ifndef SM_SMALL_FINE_BODY10
 #define SM_SMALL_FINE_BODY10 6
 #endif
+#ifndef SM_SMALL_TINY_BODY
+#define SM_SMALL_TINY_BODY 16384  // bodies up to this size (and of mostly copies): 128-byte chunks (tweet 52 -> 45 us)
+#endif
 uint32_t small_chunk(uint32_t body, uint32_t size) {
-  return (uint64_t)body * 10 <= (uint64_t)size * SM_SMALL_FINE_BODY10 && body <= (256u << 10) ? sm::kSmallChunkFine
-                                                                                               : sm::kSmallChunk;
+  if ((uint64_t)body * 10 > (uint64_t)size * SM_SMALL_FINE_BODY10 || body > (256u << 10)) return sm::kSmallChunk;
+  return body <= SM_SMALL_TINY_BODY ? sm::kSmallChunkTiny : sm::kSmallChunkFine;
 }
 constexpr uint32_t kSmallMaxOutput = 64u << 20;    // 4 B of origin pointer per output byte
 constexpr uint32_t kPinnedOutMax = 16u << 20;      // outputs the last kernel writes into the pinned staging

@@ -1344,7 +1344,8 @@ constexpr uint32_t chain_lds_bytes() {
   return 4 * kChainPool + (uint32_t)sizeof(OriginPath) * kChainPath + 2 * kLift * kChainNodes +
          (5 * 4 + 1) * kChainNodes + 4 * 5 + 2 * kJt + (kC + kIdxPad + 16) + 64 /* alignment slack */;
 }
-static_assert(chain_lds_bytes<1024>() <= 160u * 1024 && chain_lds_bytes<512>() <= 160u * 1024,
+static_assert(chain_lds_bytes<1024>() <= 160u * 1024 && chain_lds_bytes<512>() <= 160u * 1024 &&
+                  chain_lds_bytes<kSmallChunkTiny>() <= 160u * 1024,
               "k_stream_chain's LDS arrays exceed 160 KiB");
 // an entry record (exit, output) of chunk base `base`, compact: (output << 16) | (exit - base)
 __device__ inline uint32_t rec_compact(uint2 r, uint64_t base) {
@@ -1853,6 +1854,8 @@ hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint
     launch_small_front<kSmallChunk>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
   else if (chunk == kSmallChunkFine)
     launch_small_front<kSmallChunkFine>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
+  else if (chunk == kSmallChunkTiny)
+    launch_small_front<kSmallChunkTiny>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
   else
     return hipErrorInvalidValue;
   // later launches usually find nothing pending and return at once: a small grid dispatches

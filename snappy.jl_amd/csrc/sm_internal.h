@@ -58,6 +58,7 @@ constexpr uint32_t kIdxEntries = 64;  // entry offsets 0..63 covered per chunk
 // the body large (fewer chain elements).  sm_api.hip small_chunk() picks.
 constexpr uint32_t kSmallChunk = 1024;
 constexpr uint32_t kSmallChunkFine = 512;
+constexpr uint32_t kSmallChunkTiny = 128;  // small bodies of mostly copies (sm_api.hip small_chunk)
 #ifndef SM_SMALL_HOPS
 #define SM_SMALL_HOPS 1024
 #endif
