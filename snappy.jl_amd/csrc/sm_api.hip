@@ -162,24 +162,32 @@ constexpr size_t kPinnedInMax = 16u << 20;  // ... up to this size
 // runtime's pageable copy, which is 2-4 us faster there than the staging (its event and the
 // extra launch), and so does an upload through the copy engine from the staging at every size.
 // The staging is reused by the next call only after the previous upload's event.
+// the pinned input staging for n bytes, once the device is done with its previous contents (the
+// event recorded behind the last launch that read it); false: no staging
+bool stage_in_acquire(sm_ctx* ctx, size_t n) {
+  if (ctx->stage_in.ensure(n + 16) != hipSuccess || !ctx->stage_in.dp) return false;
+  return !ctx->in_ev || hipEventSynchronize(ctx->in_ev) == hipSuccess;
+}
+// after the launches that read the staging: their completion event
+hipError_t stage_in_release(sm_ctx* ctx, hipStream_t s) {
+  if (!ctx->in_ev) {
+    const hipError_t e = hipEventCreateWithFlags(&ctx->in_ev, hipEventDisableTiming);
+    if (e != hipSuccess) {
+      ctx->in_ev = nullptr;
+      return e;
+    }
+  }
+  return hipEventRecord(ctx->in_ev, s);
+}
+
 hipError_t upload_input(sm_ctx* ctx, const void* src, size_t n, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  if (n >= kPinnedInMin && n <= kPinnedInMax && ctx->stage_in.ensure(n + 16) == hipSuccess && ctx->stage_in.dp) {
-    if (!ctx->in_ev) {
-      const hipError_t e = hipEventCreateWithFlags(&ctx->in_ev, hipEventDisableTiming);
-      if (e != hipSuccess) {
-        ctx->in_ev = nullptr;
-        return e;
-      }
-    } else {
-      const hipError_t e = hipEventSynchronize(ctx->in_ev);
-      if (e != hipSuccess) return e;
-    }
+  if (n >= kPinnedInMin && n <= kPinnedInMax && stage_in_acquire(ctx, n)) {
     memcpy(ctx->stage_in.p, src, n);
     const hipError_t e = sm::launch_to_host((const uint8_t*)ctx->stage_in.dp, (uint32_t)n, (uint8_t*)ctx->in.p,
                                             nullptr, 0, nullptr, s);
     if (e != hipSuccess) return e;
-    return hipEventRecord(ctx->in_ev, s);
+    return stage_in_release(ctx, s);
   }
   return hipMemcpyAsync(ctx->in.p, src, n, hipMemcpyHostToDevice, s);
 }
@@ -228,9 +236,8 @@ int literal_uncompress(sm_ctx* ctx, const uint8_t* comp, size_t n, uint32_t size
                        uint8_t* host_out) {
   hipStream_t s = ctx->stream;
   const size_t w_off = align_up(size, 256);
-  if (ctx->stage_in.ensure(n + 16) != hipSuccess || !ctx->stage_in.dp) return 0;
   if (ctx->stage.ensure(w_off + 64) != hipSuccess || !ctx->stage.dp) return 0;
-  if (ctx->in_ev && hipEventSynchronize(ctx->in_ev) != hipSuccess) return -1;  // (a previous upload's reads)
+  if (!stage_in_acquire(ctx, n)) return 0;
   memcpy(ctx->stage_in.p, comp, n);
   uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
   volatile uint32_t* const w = (volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off);
@@ -492,7 +499,10 @@ uint32_t small_chunk(uint32_t body, uint32_t size) {
 constexpr uint32_t kSmallMaxOutput = 64u << 20;    // 4 B of origin pointer per output byte
 constexpr uint32_t kPinnedOutMax = 16u << 20;      // outputs the last kernel writes into the pinned staging
 
-int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8_t* host_out) {
+// comp: the call's input on the host.  It goes to the device through the index launch (the pinned
+// staging read there, the device copy written there); 0 returns before any launch leave
+// ctx->in without it.
+int small_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t ip0, uint32_t size, uint8_t* host_out) {
   using sm::kIdxEntries;
   const uint32_t chunk = small_chunk(n - ip0, size);
   const uint32_t nchunks = (n - ip0 + chunk - 1) / chunk;
@@ -516,12 +526,16 @@ int small_uncompress(sm_ctx* ctx, uint32_t n, uint32_t ip0, uint32_t size, uint8
   uint8_t* ib = (uint8_t*)ctx->idx.p;
   uint32_t* d_ctl = (uint32_t*)(ib + ctl_off);
   uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
+  if (!stage_in_acquire(ctx, n)) return 0;
+  memcpy(ctx->stage_in.p, comp, n);
   // the third verdict word is written by the device only when a pointer stays unresolved
   ((volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off))[2] = 0;
-  if (sm::launch_small_decode((const uint8_t*)ctx->in.p, n, ip0, size, chunk, nchunks, (uint32_t*)ib,
-                              (sm::OriginPath*)(ib + path_off), d_ctl, (uint32_t*)ctx->org.p, rounds, hops,
-                              pin_out ? sdp : (uint8_t*)ctx->out.p, (uint32_t*)(sdp + w_off), s) != hipSuccess)
+  if (sm::launch_small_decode((const uint8_t*)ctx->in.p, (const uint8_t*)ctx->stage_in.dp, n, ip0, size, chunk,
+                              nchunks, (uint32_t*)ib, (sm::OriginPath*)(ib + path_off), d_ctl,
+                              (uint32_t*)ctx->org.p, rounds, hops, pin_out ? sdp : (uint8_t*)ctx->out.p,
+                              (uint32_t*)(sdp + w_off), s) != hipSuccess)
     return -1;
+  if (stage_in_release(ctx, s) != hipSuccess) return -1;
   if (!pin_out && hipMemcpyAsync(host_out, ctx->out.p, size, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
   const volatile uint32_t* w = (const volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off);
@@ -1054,9 +1068,17 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
     const uint32_t span = (uint32_t)((SM_BLOCK_SIZE / 1024 + parts - 1) / parts);
     const size_t sl = parts > 1 ? std::max<size_t>(slot, (size_t)parts * span * sm::kSpanSlot) : slot;
     SM_CHECK(ctx->out.ensure((size_t)nfrag * sl));
-    SM_CHECK(upload_input(ctx, input, n, s));
     sm::CompressArgs a{(const uint8_t*)ctx->in.p, d_in_off, d_in_len, (uint8_t*)ctx->out.p, d_out_off, d_out_len,
                        nfrag, sm::hashtable_size(n), 0};
+    // fast modes: the screen (the first kernel) reads the input from the pinned staging and leaves
+    // the device copy the parse reads -- no separate upload
+    const bool staged = mode != SM_MODE_REFERENCE && stage_in_acquire(ctx, n);
+    if (staged) {
+      memcpy(ctx->stage_in.p, input, n);
+      a.in_host = (const uint8_t*)ctx->stage_in.dp;
+    } else {
+      SM_CHECK(upload_input(ctx, input, n, s));
+    }
     if (mode == SM_MODE_REFERENCE) {
       SM_CHECK(sm::launch_frag_plan(n, nfrag, sl, d_in_off, d_in_len, d_out_off, s));
     } else {  // (the screen, the fast modes' first kernel, writes the fragment table)
@@ -1075,6 +1097,7 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
       SM_CHECK(sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag,
                                       (uint64_t*)(sdp + t_off), sdp, s));
     }
+    if (staged) SM_CHECK(stage_in_release(ctx, s));
     SM_CHECK(hipStreamSynchronize(s));
     HT("compress (small): all")
     const volatile uint64_t* tot = (const volatile uint64_t*)((uint8_t*)ctx->stage.p + t_off);
@@ -1173,8 +1196,6 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
       }
     }
   }
-  SM_CHECK(upload_input(ctx, compressed, n, s));
-  HT("uncompress: H2D input")
   // a large stream: fragments in parallel when it is block-structured (Snappy.jl, libsnappy
   // and this library all write such streams); otherwise, or on any error, the in-order decode
   // (a body longer than its output is all literals, which the in-order engine copies HBM to HBM at
@@ -1185,7 +1206,8 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
   if (ctx->small && size >= kSmallMinOutput && size <= kSmallMaxOutput && n > hdr &&
       (uint64_t)(n - hdr) * 8 <= (uint64_t)size * SM_SMALL_BODY8 &&
       (n - hdr + sm::kSmallChunk - 1) / sm::kSmallChunk <= kSmallMaxChunks) {
-    const int r = small_uncompress(ctx, (uint32_t)n, (uint32_t)hdr, size, (uint8_t*)uncompressed);
+    const int r = small_uncompress(ctx, (const uint8_t*)compressed, (uint32_t)n, (uint32_t)hdr, size,
+                                   (uint8_t*)uncompressed);
     if (r < 0) return SM_ERR_DEVICE;
     if (r == 4) {
       ctx->last_path = 4;
@@ -1193,6 +1215,9 @@ sm_status sm_uncompress(sm_ctx* ctx, const char* compressed, size_t n, char* unc
       return SM_OK;
     }
   }
+  // (path 4 uploads through its index launch; every other path from here)
+  SM_CHECK(upload_input(ctx, compressed, n, s));
+  HT("uncompress: H2D input")
   if (size >= kParallelMinOutput && n - hdr >= 2 * sm::kIdxChunk) {
     bool copied = false;
     int32_t err = SM_OK;

@@ -92,6 +92,15 @@ __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) 
   }
   const uint8_t* src = a.in + ioff;
   uint8_t* dst = a.out + ooff;
+  if (a.in_host && n <= kBlockSize) {  // the upload folded in: this block's bytes to the device copy
+    src = a.in_host + ioff;
+    uint8_t* const d = const_cast<uint8_t*>(a.in) + ioff;
+    const bool al = (((uintptr_t)src | (uintptr_t)d) & 15) == 0;
+    const uint32_t n16 = al ? n >> 4 : 0u;
+    for (uint32_t k = tid; k < n16; k += kScrThreads)
+      reinterpret_cast<uint4*>(d)[k] = reinterpret_cast<const uint4*>(src)[k];
+    for (uint32_t k = 16 * n16 + tid; k < n; k += kScrThreads) d[k] = src[k];
+  }
   if (n < kScrMinLen || n > kBlockSize) {
     if (tid == 0) a.out_len[b] = kScreenTodo;
     return;

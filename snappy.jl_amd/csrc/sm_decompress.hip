@@ -852,9 +852,13 @@ __device__ inline void dev_walk(const uint8_t* __restrict__ in, uint32_t N, uint
 // kDeep: one wave per deep-record chain (kDeepChains waves): wave 0 indexes the chunk, then each
 // wave walks its chain's levels (serial dev_walks) at the same time as the others.
 constexpr uint32_t index_threads(bool deep) { return deep ? kDeepChains * kWave : kWave; }
+// copy_to (path 4 from a host call, else null): `in` is the call's input in device-mapped pinned
+// host memory, and chunk c's bytes (chunk 0: also the header before ip0) go on to copy_to, the
+// device copy the later kernels read -- the upload folded into the index launch.
 template <uint32_t kC, bool kDeep>  // compressed bytes per chunk (kIdxChunk; path 4: kSmallChunk)
 __global__ __launch_bounds__(index_threads(kDeep)) void k_stream_index(const uint8_t* __restrict__ in, uint32_t N,
-                                                                          uint32_t ip0, uint2* rec, uint4* deep) {
+                                                                          uint32_t ip0, uint2* rec, uint4* deep,
+                                                                          uint8_t* __restrict__ copy_to) {
   __shared__ __attribute__((aligned(16))) uint8_t buf[kC + kIdxPad];
   __shared__ __attribute__((aligned(16))) uint16_t jt[6 * 256];  // walk tables, then the entry walk's 3 KiB
   __shared__ uint32_t bm[kC / 32];  // positions on lane 0's path
@@ -865,6 +869,10 @@ __global__ __launch_bounds__(index_threads(kDeep)) void k_stream_index(const uin
   __shared__ uint64_t xs[kDeepChains];  // each chain's first entry (~0: none)
   const uint32_t c = blockIdx.x, lane = lane_id(), wv = threadIdx.x / kWave;
   const uint32_t s = ip0 + c * kC;
+  if (copy_to) {
+    const uint32_t a = c == 0 ? 0u : s, e = min(s + kC, N);
+    for (uint32_t k = a + threadIdx.x; k < e; k += blockDim.x) copy_to[k] = in[k];
+  }
   if (wv == 0) {  // (one wave from here to the chain starts: LDS in order, signal fences only)
     stage_bytes(buf, in, N, s, kC + kIdxPad, lane);
     for (uint32_t k = lane; k < kC / 32; k += kWave) bm[k] = 0;
@@ -1835,27 +1843,29 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
 }
 
 template <uint32_t kC>
-static void launch_small_front(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t nchunks, uint32_t* rec,
-                               OriginPath* path, uint32_t* ctl, uint32_t* P, uint32_t rounds, hipStream_t s) {
+static void launch_small_front(const uint8_t* in, const uint8_t* in_host, uint32_t N, uint32_t ip0, uint32_t size,
+                               uint32_t nchunks, uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P,
+                               uint32_t rounds, hipStream_t s) {
   uint4* deep = reinterpret_cast<uint4*>(rec + (size_t)nchunks * kIdxEntries * 2);  // kDeepChains x kDeepLevels per chunk
-  hipLaunchKernelGGL((k_stream_index<kC, true>), dim3(nchunks), dim3(index_threads(true)), 0, s, in, N, ip0,
-                     reinterpret_cast<uint2*>(rec), deep);
+  // (in_host: the index launch reads the input there and leaves its device copy at in)
+  hipLaunchKernelGGL((k_stream_index<kC, true>), dim3(nchunks), dim3(index_threads(true)), 0, s, in_host ? in_host : in,
+                     N, ip0, reinterpret_cast<uint2*>(rec), deep, in_host ? const_cast<uint8_t*>(in) : nullptr);
   hipLaunchKernelGGL(k_stream_chain<kC>, dim3(1), dim3(kChainThreads), 0, s, in, N, ip0, size, nchunks,
                      reinterpret_cast<const uint2*>(rec), deep, path, ctl, rounds);
   hipLaunchKernelGGL(k_origin_fill_dev<kC>, dim3(nchunks), dim3(64), 0, s, in, N, size, path, P, ctl);
 }
 
-hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t chunk,
+hipError_t launch_small_decode(const uint8_t* in, const uint8_t* in_host, uint32_t N, uint32_t ip0, uint32_t size, uint32_t chunk,
                                uint32_t nchunks, uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P,
                                uint32_t rounds, uint32_t hops, uint8_t* out, uint32_t* words, hipStream_t s) {
   if (nchunks == 0 || size == 0 || rounds == 0 || 4 + rounds > kWave || hops == 0 || hops > kOneLaunchHops)
     return hipErrorInvalidValue;
   if (chunk == kSmallChunk)
-    launch_small_front<kSmallChunk>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
+    launch_small_front<kSmallChunk>(in, in_host, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
   else if (chunk == kSmallChunkFine)
-    launch_small_front<kSmallChunkFine>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
+    launch_small_front<kSmallChunkFine>(in, in_host, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
   else if (chunk == kSmallChunkTiny)
-    launch_small_front<kSmallChunkTiny>(in, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
+    launch_small_front<kSmallChunkTiny>(in, in_host, N, ip0, size, nchunks, rec, path, ctl, P, rounds, s);
   else
     return hipErrorInvalidValue;
   // later launches usually find nothing pending and return at once: a small grid dispatches
@@ -1877,7 +1887,7 @@ hipError_t launch_stream_index(const uint8_t* in, uint32_t N, uint32_t ip0, uint
                                hipStream_t s) {
   if (nchunks == 0) return hipSuccess;
   hipLaunchKernelGGL((k_stream_index<kIdxChunk, false>), dim3(nchunks), dim3(64), 0, s, in, N, ip0,
-                     reinterpret_cast<uint2*>(rec), nullptr);
+                     reinterpret_cast<uint2*>(rec), nullptr, nullptr);
   return hipGetLastError();
 }
 

@@ -24,6 +24,9 @@ struct CompressArgs {
   // (instead of a k_frag_plan launch) before the kernels after it read them
   uint64_t plan_n = 0;
   uint64_t plan_slot = 0;
+  // in_host != null (sm_compress, fast modes): the input in device-mapped pinned host memory; the
+  // screen reads its block there and writes the device copy at `in`, which the parse reads
+  const uint8_t* in_host = nullptr;
 };
 
 struct DecompressArgs {
@@ -104,7 +107,9 @@ hipError_t launch_origin_resolve(uint32_t* P, uint32_t size, uint32_t* pending, 
 // bytes in the launch that resolves it) and words[0..1] = ctl[1], ctl[2]; the last launch sets
 // words[2] = 1 when a pointer is still unresolved after it (the caller zeroes words[2] first).  Any
 // nonzero word: fall back.  out and words may be device-mapped pinned host memory.
-hipError_t launch_small_decode(const uint8_t* in, uint32_t N, uint32_t ip0, uint32_t size, uint32_t chunk,
+// in_host (nullable): the input in device-mapped pinned host memory -- the index launch reads it
+// there and writes the device copy at in, which the later launches read (no separate upload).
+hipError_t launch_small_decode(const uint8_t* in, const uint8_t* in_host, uint32_t N, uint32_t ip0, uint32_t size, uint32_t chunk,
                                uint32_t nchunks, uint32_t* rec, OriginPath* path, uint32_t* ctl, uint32_t* P,
                                uint32_t rounds, uint32_t hops, uint8_t* out, uint32_t* words, hipStream_t s);
 // src[0, n) to dst and wsrc[0, nw) to words by a kernel (dst, words: device-mapped pinned host
