@@ -490,11 +490,19 @@ constexpr uint32_t kSmallMaxChunks = (1u << 20) / sm::kSmallChunk;  // compresse
 #define SM_SMALL_FINE_BODY10 6
 #endif
 #ifndef SM_SMALL_TINY_BODY
-#define SM_SMALL_TINY_BODY 16384  // bodies up to this size (and of mostly copies): 128-byte chunks (tweet 52 -> 45 us)
+#define SM_SMALL_TINY_BODY 16384  // bodies up to this size ...
 #endif
+#ifndef SM_SMALL_TINY_BODY10
+#define SM_SMALL_TINY_BODY10 9    // ... and at most this many tenths of the output: 128-byte chunks
+#endif
+// path 4's index chunk: 128 bytes for small bodies with copies (sample-tweet.json 52 -> 45 us, 4-16
+// KiB of text 51-56 -> 45-48 us), 512 for bodies of mostly copies, else 1024 (literal-rich
+// streams, where finer chunks lengthen the chain: paper-100k.pdf 137 -> 168 us at 512)
 uint32_t small_chunk(uint32_t body, uint32_t size) {
+  if (body <= SM_SMALL_TINY_BODY && (uint64_t)body * 10 <= (uint64_t)size * SM_SMALL_TINY_BODY10)
+    return sm::kSmallChunkTiny;
   if ((uint64_t)body * 10 > (uint64_t)size * SM_SMALL_FINE_BODY10 || body > (256u << 10)) return sm::kSmallChunk;
-  return body <= SM_SMALL_TINY_BODY ? sm::kSmallChunkTiny : sm::kSmallChunkFine;
+  return sm::kSmallChunkFine;
 }
 constexpr uint32_t kSmallMaxOutput = 64u << 20;    // 4 B of origin pointer per output byte
 constexpr uint32_t kPinnedOutMax = 16u << 20;      // outputs the last kernel writes into the pinned staging
