@@ -999,11 +999,18 @@ def test_uncompress_small_streams_device_path(sm, oracle, libsnappy, gpu_availab
                 assert out_g == out_o
 
 
-def _fine_chunks(sm, s):
-    """sm_api.hip small_chunk(): 512-byte index chunks for bodies <= 0.6 of the output and 256 KiB."""
+def _chunk_of(sm, s):
+    """sm_api.hip small_chunk(): 128-byte index chunks for bodies <= 16 KiB and <= 0.9 of the
+    output, 512 for bodies <= 0.6 of the output and 256 KiB, else 1024."""
     size, hdr = sm.parse32(s)
     body = len(s) - hdr
-    return body * 10 <= size * 6 and body <= 256 << 10
+    if body <= 16384 and body * 10 <= size * 9:
+        return 128
+    return 512 if body * 10 <= size * 6 and body <= 256 << 10 else 1024
+
+
+def _fine_chunks(sm, s):
+    return _chunk_of(sm, s) < 1024
 
 
 def test_small_path_chunk_sizes_and_parallel_runs(sm, oracle, gpu_available):
@@ -1047,6 +1054,55 @@ def test_small_path_chunk_sizes_and_parallel_runs(sm, oracle, gpu_available):
     assert sum(small_path(sm, s) for s, _ in cases) >= len(cases) - 2
     for s, _ in cases[-3:]:
         for _ in range(10):
+            bad = bytearray(s)
+            bad[int(rng.integers(2, len(bad)))] = int(rng.integers(0, 256))
+            bad = bytes(bad)
+            st_o, out_o = oracle.uncompress_status(bad)
+            try:
+                st_g, out_g = 0, sm.uncompress(bad)
+            except sm.SnappyError as exc:
+                st_g, out_g = exc.code, None
+            assert st_g == st_o
+            if st_o == 0:
+                assert out_g == out_o
+
+
+def test_small_path_tiny_chunks(sm, oracle, gpu_available):
+    """Path 4 with 128-byte index chunks (round 6): bodies of 1, 2 and many chunks up to the 16 KiB
+    bound and past it, ratios on both sides of 0.9, copy runs across chunk boundaries, long
+    literals that enter chunks deep (deep records at 128 bytes), and mutations: output and
+    status equal the oracle's, and the chunk rule picks 128 where it says so."""
+    from streams import build
+    rng = np.random.default_rng(128)
+    cases = []
+    for body in (4000, 4096, 8000, 16384, 16385):
+        for lit_share in (0.05, 0.3, 0.6):  # the literal bytes' share of the output
+            ops, size, b = [], 0, 0
+            while b < body - 80:
+                if rng.random() < lit_share:
+                    n = int(rng.integers(1, 300))
+                    ops.append(("lit", rng.integers(0, 256, n, dtype=np.uint8).tobytes()))
+                    size += n
+                    b += n + (1 if n <= 60 else 2 if n <= 256 else 3)
+                elif size >= 4:
+                    L = int(rng.integers(4, 65))
+                    ops.append(("copy", int(rng.integers(1, min(size, 2000) + 1)), L))
+                    size += L
+                    b += 3
+                else:
+                    ops.append(("lit", rng.integers(0, 256, 8, dtype=np.uint8).tobytes()))
+                    size += 8
+                    b += 9
+            cases.append(build(ops))
+    chunks = [_chunk_of(sm, s) for s, _ in cases]
+    assert 128 in chunks and any(c != 128 for c in chunks), chunks
+    for s, e in cases:
+        assert oracle.uncompress(s) == e
+        assert sm.uncompress(s) == e, len(e)
+        if small_path(sm, s):
+            assert sm.last_uncompress_path() == 4
+    for s, _ in cases[::3]:
+        for _ in range(6):
             bad = bytearray(s)
             bad[int(rng.integers(2, len(bad)))] = int(rng.integers(0, 256))
             bad = bytes(bad)
