@@ -321,6 +321,13 @@ def kernel_ms(fn, reps):
     return float(np.median([s.elapsed_time(e) for s, e in ev]))
 
 
+# compressed bytes each decode launch reads (set by main): the decoders' FETCH_SIZE splits into
+# that stream, read once by coalesced 4-byte lanes (raw FETCH = 1/2 of the bytes, as the guide's
+# wide reads), and far-copy sources and window reloads, 16-64-byte gathers whose raw FETCH is the
+# 64-byte sectors they move (tools/probes/fetch_calib.hip, profiles/r06_fetch_calibration.txt)
+DECODE_STREAM_BYTES = {}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch from the round's PMC file (rocprofv3 FETCH_SIZE/WRITE_SIZE passes, run
     separately from this process: counters cannot be collected inside a timed run), with where
@@ -338,7 +345,16 @@ def pmc_traffic(kernel):
         cur = None
     src = {"file": rel, "library": lib, "commit": d.get("commit"), "this_run_library": cur,
            "same_build": bool(lib) and lib == cur}
-    return d.get(kernel, {}).get("hbm_bytes_per_launch"), src
+    e = d.get(kernel, {})
+    cstream = DECODE_STREAM_BYTES.get(kernel)
+    if cstream is not None and "fetch_size_bytes_raw" in e:
+        raw, wr = e["fetch_size_bytes_raw"], e["write_size_bytes"]
+        rest = max(raw - cstream / 2.0, 0.0)
+        src["calibrated"] = {"hbm_bytes_per_launch": round(cstream + rest + wr),
+                             "stream_read": cstream, "gathers_and_reloads": round(rest), "written": wr,
+                             "rule": "stream raw x2, gathers raw x1 (profiles/r06_fetch_calibration.txt); "
+                                     "`traffic` applies x2 to all of FETCH (the guide's wide-read rule)"}
+    return e.get("hbm_bytes_per_launch"), src
 
 
 # the rocprof kernels behind each timed call (a fast-mode compress is the incompressible screen
@@ -581,6 +597,7 @@ def main():
     elapsed = timed_steps(step, args.steps, args.warmup, world, dist, dev)
     headline_sizes = batch.comp_len.clone()
     comp_bytes = batch.comp_bytes()
+    DECODE_STREAM_BYTES["uncompress"] = comp_bytes
     in_bytes = batch.in_bytes
     t_c = kernel_ms(lambda: batch.compress(sm), reps)
     t_d = kernel_ms(lambda: batch.uncompress(sm), reps)
@@ -596,6 +613,7 @@ def main():
     # them against the oracle block for block); reported beside the headline, not in it
     t_ref = kernel_ms(lambda: batch.compress(sm, "reference"), 3)
     ref_comp = batch.comp_bytes()
+    DECODE_STREAM_BYTES["uncompress_reference_streams"] = ref_comp
     # config 3's other half: the decode of the reference-mode (Snappy.jl's own)
     # streams of the same blocks, with its own roofline
     t_rd = kernel_ms(lambda: batch.uncompress(sm), reps)
@@ -629,6 +647,7 @@ def main():
             rb.uncompress(sm)
         r_el = timed_steps(rstep, args.steps, args.warmup, world, dist, dev)
         rc_bytes = rb.comp_bytes()
+        DECODE_STREAM_BYTES["uncompress_random"] = rc_bytes
         rt_c = kernel_ms(lambda: rb.compress(sm), reps)
         rt_d = kernel_ms(lambda: rb.uncompress(sm), reps)
         r_ok = rb.verify()
