@@ -142,6 +142,7 @@ constexpr uint32_t kBatchOut = SM_DEC_BOUT;  // most output bytes of one batch
 constexpr uint32_t kKeep = SM_DEC_KEEP;  // bytes a shift keeps (the least LDS source reach)
 constexpr uint32_t kWinPad = 16;         // bytes before the window (the dword below a piece)
 static_assert(kKeep + 15 + kBatchOut + 32 <= kWin && kKeep >= 80 && kWin % 16 == 0, "window bounds");
+static_assert(kKeep + 15 <= 16 * kWave, "win_shift moves at most one 16-byte unit per lane");
 
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
