@@ -80,6 +80,7 @@ static_assert(kScC == 16 && kScG == 16, "a lane's 16 positions: one u16 mask, on
 #ifndef SC_FAR  // fast mode: the older of two matching candidates when the recent one is nearer
 #define SC_FAR 256
 #endif
+constexpr uint32_t kMaskPasses = 16;  // resync passes that may use the covered-lane proposal (the loop)
 #ifndef SC_WPRIO
 #define SC_WPRIO 3
 #endif
@@ -604,16 +605,43 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     walk(std::false_type{}, row ? 0u : 16u, 0u, P, mp, e);
     if (!row) e = c0;
   }
-  for (;;) {
+  for (uint32_t pass = 0;; ++pass) {
     // every lane's start: the furthest end of the lanes before it (an exclusive max-scan), not only
     // the previous lane's -- a copy that covers several rows reaches every covered lane in one round
     // instead of one lane a round.  The fixed point is the same (ends are non-decreasing there, so
     // the max is the previous lane's end), so are the bytes; config 5's corpus 2.478 -> 2.367 ms,
     // the bench text unchanged
     const uint32_t pe = __builtin_amdgcn_update_dpp(0u, scan_max_dpp(e), 0x138, 0xf, 0xf, false);  // wave_shr:1
-    const uint32_t sn = lane == 0 ? sc0 : pe;
-    const bool chg = sn != s;
-    if (!ballot(chg)) break;
+    const uint32_t st = lane == 0 ? sc0 : pe;
+    uint32_t sn = st;
+    // A lane whose start is past its row is covered: it forwards that start, and its own end (from
+    // an earlier walk) is stale.  Stale ends only overestimate, and fed to the scan they push every
+    // later lane too far, so data of long matches corrected one row a pass (geo.protodata 13.8
+    // passes a super-chunk, a 427-byte period 50).  The proposal leaves covered lanes out of the
+    // scan (a few cheap scans, until the covered set is stable).  The loop still ends only where
+    // the plain scan agrees (the unique fixed point: the bytes are unchanged), takes the plain
+    // scan's starts whenever the proposal changes nothing, and after kMaskPasses passes uses the
+    // plain rule alone (which settles lane k by pass k + 1).  Same bytes on every corpus file and
+    // the bench sets (tools/ab_bytes.py); config 5's fragments 2.369 -> 2.267 ms, geo.protodata
+    // 2,000 windows 0.750 -> 0.584, the bench text 2.020 -> 2.036 (profiles/r06_ab_experiments.txt)
+    if (pass < kMaskPasses) {
+      uint64_t cov = ballot(st >= ce);
+      for (int it = 0; cov && it < 3; ++it) {
+        const uint32_t x = sn >= ce ? 0u : e;
+        const uint32_t pm = __builtin_amdgcn_update_dpp(0u, scan_max_dpp(x), 0x138, 0xf, 0xf, false);
+        sn = lane == 0 ? sc0 : pm;
+        const uint64_t c = ballot(sn >= ce);
+        if (c == cov) break;
+        cov = c;
+      }
+    }
+    bool chg = sn != s;
+    if (!ballot(chg)) {
+      if (!ballot(st != s)) break;  // the fixed point of the plain rule
+      sn = st;
+      chg = st != s;
+    }
+
     const bool inrow = chg && sn < ce;  // (an entry is never before the row)
     uint32_t nP, mp, ne;
     walk(std::true_type{}, inrow ? sn - c0 : 16u, P, nP, mp, ne);  // (rows not walking: stop at once)
