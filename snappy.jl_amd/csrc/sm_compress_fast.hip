@@ -28,6 +28,7 @@ constexpr uint32_t kScreenTodo = 0xfffffffeu;  // out_len mark of k_literal_scre
 // and a block with fewer than kScrMin repeated anchors has ~kScrMin x 64 B of repeats at most.
 constexpr uint32_t kScrMin = 8;           // repeated anchors that make a block "compressible"
 constexpr uint32_t kScrMinLen = 8192;     // smaller blocks always take the parse
+constexpr uint32_t kScrAnchorDiv = 256;   // fewer than one anchor per 256 bytes scanned: not random (expected: 1 per 64)
 #ifndef SM_SCR_THREADS
 #define SM_SCR_THREADS 512
 #endif
@@ -53,7 +54,8 @@ __device__ inline uint4 scr_load16(const uint8_t* src, uint32_t o, uint32_t n, b
 
 // repeated anchors among the 16 positions of a piece v (bytes [o, o + 16)), nv = the next piece
 // (valid = its first 3 bytes are real: the positions 13..15 have their 4 bytes)
-__device__ inline uint32_t scr_anchors(uint32_t* tab, uint4 v, uint4 nv, uint32_t o, uint32_t n, bool nvalid) {
+__device__ inline uint32_t scr_anchors(uint32_t* tab, uint4 v, uint4 nv, uint32_t o, uint32_t n, bool nvalid,
+                                       uint32_t& anc) {
   const uint32_t x[5] = {v.x, v.y, v.z, v.w, nv.x};
   uint32_t rep = 0;
 #pragma unroll
@@ -64,6 +66,7 @@ __device__ inline uint32_t scr_anchors(uint32_t* tab, uint4 v, uint4 nv, uint32_
     if (ok && (h >> 26) == 0) {
       const uint32_t old = atomicExch(&tab[(h >> 14) & ((1u << kScrTabBits) - 1)], w);
       rep += old == w ? 1u : 0u;
+      ++anc;
     }
   }
   return rep;
@@ -71,7 +74,7 @@ __device__ inline uint32_t scr_anchors(uint32_t* tab, uint4 v, uint4 nv, uint32_
 
 __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) {
   __shared__ uint32_t tab[1u << kScrTabBits];
-  __shared__ uint32_t cnt[2];
+  __shared__ uint32_t cnt[4];  // repeated anchors (first pass, rest), anchors (first pass, rest)
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t b = blockIdx.x;
   uint32_t n;
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) 
   }
   const bool aligned = ((uintptr_t)src & 15) == 0;
   for (uint32_t k = tid; k < (1u << kScrTabBits); k += kScrThreads) tab[k] = kScrEmpty;
-  if (tid < 2) cnt[tid] = 0;
+  if (tid < 4) cnt[tid] = 0;
   uint4 v[kScrPieces];
 #pragma unroll
   for (uint32_t i = 0; i < kScrPieces; ++i) v[i] = make_uint4(0, 0, 0, 0);
@@ -117,15 +120,17 @@ __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) 
 #pragma unroll
     for (uint32_t i = i0; i < i1; ++i) v[i] = scr_load16(src, 16 * (tid + kScrThreads * i), n, aligned);
     __syncthreads();  // (the table is initialised)
-    uint32_t rep = 0;
+    uint32_t rep = 0, anc = 0;
 #pragma unroll
     for (uint32_t i = i0; i < i1; ++i) {
       uint4 nv;
       nv.x = __builtin_amdgcn_update_dpp(0u, v[i].x, 0x130, 0xf, 0xf, false);  // wave_shl:1
-      rep += scr_anchors(tab, v[i], nv, 16 * (tid + kScrThreads * i), n, lane < 63);
+      rep += scr_anchors(tab, v[i], nv, 16 * (tid + kScrThreads * i), n, lane < 63, anc);
     }
     rep = __builtin_amdgcn_readlane(scan_dpp(rep), 63);
+    anc = __builtin_amdgcn_readlane(scan_dpp(anc), 63);
     if (lane == 0 && rep) atomicAdd(&cnt[slot], rep);
+    if (lane == 0 && anc) atomicAdd(&cnt[2 + slot], anc);
     __syncthreads();
   };
   pass(0, kScrFirst, 0);
@@ -134,7 +139,12 @@ __global__ __launch_bounds__(kScrThreads) void k_literal_screen(CompressArgs a) 
     return;
   }
   if (n > 16 * kScrThreads * kScrFirst) pass(kScrFirst, kScrPieces, 1);
-  if (cnt[0] + cnt[1] >= kScrMin) {
+  // Too few anchors for the bytes scanned (random data has one per 64 positions: ~1,024 in a
+  // block) means few distinct words -- a constant run or a short period, whose words may all miss
+  // the anchor range -- not random data: that block goes to the parse too (a constant 64 KiB
+  // block was one 65,542-byte literal, against the reference's 3,077 bytes).
+  const uint32_t scanned = min(n, n > 16 * kScrThreads * kScrFirst ? kBlockSize : 16 * kScrThreads * kScrFirst);
+  if (cnt[0] + cnt[1] >= kScrMin || (cnt[2] + cnt[3]) * kScrAnchorDiv < scanned) {
     if (tid == 0) a.out_len[b] = kScreenTodo;
     return;
   }

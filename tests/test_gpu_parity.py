@@ -1159,6 +1159,42 @@ def test_single_calls_through_pinned_staging(sm, oracle, gpu_available):
             assert _status(sm, bad) == oracle.uncompress_status(bad)
 
 
+@pytest.mark.parametrize("mode", FAST_MODES)
+def test_fast_mode_periodic_blocks(sm, oracle, gpu_available, mode):
+    """Periodic blocks (sm_compress_sc.hip's resync on long matches: every row's first walk ends
+    in a long extended copy, most of them covered by an earlier row's; the masked proposal and its
+    plain-rule fallback must reach the same fixed point): periods 1..4096, some with mutations,
+    batched and as single calls in parts; every stream decodes under the oracle, parts equal the
+    whole-block parse, and a repeated launch gives the same bytes."""
+    rng = np.random.default_rng(0x9E7)
+    blocks = []
+    for per in (1, 2, 3, 7, 16, 17, 31, 64, 100, 255, 256, 427, 1000, 1023, 4096):
+        base = rng.integers(0, 256, per, dtype=np.uint8)
+        blk = np.tile(base, 65536 // per + 1)[:65536].copy()
+        blocks.append(blk.tobytes())
+        mut = blk.copy()
+        for q in rng.integers(0, 65536, 40):
+            mut[q] = rng.integers(0, 256)
+        blocks.append(mut.tobytes())
+    out = sm.compress_batch(blocks, mode=mode)
+    assert out == sm.compress_batch(blocks, mode=mode)
+    for raw, comp in zip(blocks, out):
+        assert oracle.uncompress(comp) == raw
+        # (no literal fallback on low-entropy blocks: within 10% of the reference's size -- a
+        # mutated constant block is 1.064x, copies of 64 split at other offsets than the reference's)
+        assert len(comp) <= len(oracle.compress(raw)) * 1.10 + 64
+    try:
+        for raw in blocks[::3]:
+            sm.set_split_compress(False)
+            whole = sm.compress(raw, mode=mode)
+            sm.set_split_compress(True)
+            parts = sm.compress(raw, mode=mode)
+            assert parts == whole
+            assert oracle.uncompress(parts) == raw
+    finally:
+        sm.set_split_compress(True)
+
+
 @pytest.mark.parametrize("mode", ["fast", "dense"])
 def test_compress_in_parts_equals_whole_block_parse(sm, oracle, gpu_available, mode):
     """compress() of small inputs parses each 64 KiB fragment in parts on their own workgroups

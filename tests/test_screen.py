@@ -94,7 +94,9 @@ def test_literal_copy_every_alignment(sm, oracle, gpu_available, header):
 
 
 def test_screen_keeps_compressible_blocks(sm, oracle, gpu_available):
-    """Text, structured data, half-random/half-text and runs take the parse (smaller than the input)."""
+    """Text, structured data, half-random/half-text and runs take the parse (smaller than the input);
+    so do constant blocks and short periods whose few distinct words all miss the anchor range
+    (round 6: a block of 0x14 bytes was emitted as one literal -- too few anchors for random data)."""
     from conftest import read_testfile
     rng = np.random.default_rng(7)
     text = read_testfile("alice29.txt")[:65536]
@@ -103,7 +105,9 @@ def test_screen_keeps_compressible_blocks(sm, oracle, gpu_available):
     mixed = rnd[:32768] + text[:32768]
     zeros_tail = rnd[:49152] + bytes(16384)
     blocks = [text, geo, mixed, zeros_tail, bytes(65536)]
-    out, out_off, lens = _run(sm, blocks, [0] * 5, [0] * 5, True)
+    blocks += [bytes([c]) * 65536 for c in (0x14, 0x20, 0x41, 0x7f, 0xff)]
+    blocks += [(bytes(rng.integers(0, 256, per, dtype=np.uint8)) * (65536 // per + 1))[:65536] for per in (2, 3, 5, 12)]
+    out, out_off, lens = _run(sm, blocks, [0] * len(blocks), [0] * len(blocks), True)
     for b, blk in enumerate(blocks):
         s = out[out_off[b]:out_off[b] + lens[b]].tobytes()
         assert oracle.uncompress(s) == blk
