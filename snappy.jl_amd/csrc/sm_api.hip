@@ -538,12 +538,14 @@ int small_uncompress(sm_ctx* ctx, const uint8_t* comp, uint32_t n, uint32_t ip0,
   memcpy(ctx->stage_in.p, comp, n);
   // the third verdict word is written by the device only when a pointer stays unresolved
   ((volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off))[2] = 0;
-  if (sm::launch_small_decode((const uint8_t*)ctx->in.p, (const uint8_t*)ctx->stage_in.dp, n, ip0, size, chunk,
-                              nchunks, (uint32_t*)ib, (sm::OriginPath*)(ib + path_off), d_ctl,
-                              (uint32_t*)ctx->org.p, rounds, hops, pin_out ? sdp : (uint8_t*)ctx->out.p,
-                              (uint32_t*)(sdp + w_off), s) != hipSuccess)
+  const hipError_t le = sm::launch_small_decode((const uint8_t*)ctx->in.p, (const uint8_t*)ctx->stage_in.dp, n, ip0,
+                                                size, chunk, nchunks, (uint32_t*)ib, (sm::OriginPath*)(ib + path_off),
+                                                d_ctl, (uint32_t*)ctx->org.p, rounds, hops,
+                                                pin_out ? sdp : (uint8_t*)ctx->out.p, (uint32_t*)(sdp + w_off), s);
+  if (le != hipSuccess || stage_in_release(ctx, s) != hipSuccess) {
+    (void)hipStreamSynchronize(s);  // (no launch may still read the staging when the call returns)
     return -1;
-  if (stage_in_release(ctx, s) != hipSuccess) return -1;
+  }
   if (!pin_out && hipMemcpyAsync(host_out, ctx->out.p, size, hipMemcpyDeviceToHost, s) != hipSuccess) return -1;
   if (hipStreamSynchronize(s) != hipSuccess) return -1;
   const volatile uint32_t* w = (const volatile uint32_t*)((uint8_t*)ctx->stage.p + w_off);
@@ -1095,17 +1097,22 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
     }
     // the gather writes the body and its (length, error) pair straight into the pinned staging
     uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
-    if (parts > 1) {
-      const sm::ScSpan sp{parts, span, (uint64_t)span * sm::kSpanSlot, d_part_len};
-      SM_CHECK(sm::launch_compress_span(a, mode, sp, s));
+    const sm::ScSpan sp{parts, span, (uint64_t)span * sm::kSpanSlot, d_part_len};
+    hipError_t le = parts > 1 ? sm::launch_compress_span(a, mode, sp, s) : sm::launch_compress(a, mode, s);
+    if (staged) {  // (the screen, the staging's only reader, may be queued even when a later launch failed)
+      const hipError_t re = stage_in_release(ctx, s);
+      if (le == hipSuccess) le = re;
+    }
+    if (le != hipSuccess) {
+      (void)hipStreamSynchronize(s);
+      return SM_ERR_DEVICE;
+    }
+    if (parts > 1)
       SM_CHECK(sm::launch_parts_gather((const uint8_t*)ctx->out.p, d_out_off, sp, (const uint8_t*)ctx->in.p,
                                        d_in_off, d_in_len, nfrag, (uint64_t*)(sdp + t_off), sdp, s));
-    } else {
-      SM_CHECK(sm::launch_compress(a, mode, s));
+    else
       SM_CHECK(sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag,
                                       (uint64_t*)(sdp + t_off), sdp, s));
-    }
-    if (staged) SM_CHECK(stage_in_release(ctx, s));
     SM_CHECK(hipStreamSynchronize(s));
     HT("compress (small): all")
     const volatile uint64_t* tot = (const volatile uint64_t*)((uint8_t*)ctx->stage.p + t_off);
