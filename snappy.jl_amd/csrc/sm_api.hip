@@ -1099,7 +1099,14 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
     uint8_t* const sdp = (uint8_t*)ctx->stage.dp;
     const sm::ScSpan sp{parts, span, (uint64_t)span * sm::kSpanSlot, d_part_len};
     hipError_t le = parts > 1 ? sm::launch_compress_span(a, mode, sp, s) : sm::launch_compress(a, mode, s);
-    if (staged) {  // (the screen, the staging's only reader, may be queued even when a later launch failed)
+    if (le == hipSuccess)
+      le = parts > 1 ? sm::launch_parts_gather((const uint8_t*)ctx->out.p, d_out_off, sp, (const uint8_t*)ctx->in.p,
+                                               d_in_off, d_in_len, nfrag, (uint64_t*)(sdp + t_off), sdp, s)
+                     : sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag,
+                                              (uint64_t*)(sdp + t_off), sdp, s);
+    // the staging's release after the last launch (an event between the launches costs each call
+    // ~4 us), and recorded even when a launch failed: the screen, its only reader, may be queued
+    if (staged) {
       const hipError_t re = stage_in_release(ctx, s);
       if (le == hipSuccess) le = re;
     }
@@ -1107,12 +1114,6 @@ sm_status sm_compress(sm_ctx* ctx, const char* input, size_t n, char* compressed
       (void)hipStreamSynchronize(s);
       return SM_ERR_DEVICE;
     }
-    if (parts > 1)
-      SM_CHECK(sm::launch_parts_gather((const uint8_t*)ctx->out.p, d_out_off, sp, (const uint8_t*)ctx->in.p,
-                                       d_in_off, d_in_len, nfrag, (uint64_t*)(sdp + t_off), sdp, s));
-    else
-      SM_CHECK(sm::launch_frag_gather((const uint8_t*)ctx->out.p, d_out_off, d_out_len, d_in_len, nfrag,
-                                      (uint64_t*)(sdp + t_off), sdp, s));
     SM_CHECK(hipStreamSynchronize(s));
     HT("compress (small): all")
     const volatile uint64_t* tot = (const volatile uint64_t*)((uint8_t*)ctx->stage.p + t_off);
