@@ -622,8 +622,11 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
     // the plain scan agrees (the unique fixed point: the bytes are unchanged), takes the plain
     // scan's starts whenever the proposal changes nothing, and after kMaskPasses passes uses the
     // plain rule alone (which settles lane k by pass k + 1).  Same bytes on every corpus file and
-    // the bench sets (tools/ab_bytes.py); config 5's fragments 2.369 -> 2.267 ms, geo.protodata
-    // 2,000 windows 0.750 -> 0.584, the bench text 2.020 -> 2.036 (profiles/r06_ab_experiments.txt)
+    // the bench sets (tools/ab_bytes.py); config 5's fragments 2.369 -> 2.258 ms, geo.protodata
+    // 2,000 windows 0.750 -> 0.584, the bench text 2.020 -> 2.033 (the proposal after the plain
+    // fixed-point test, so the last pass does not pay for it: profiles/r06_ab_experiments.txt)
+    bool chg = st != s;
+    if (!ballot(chg)) break;  // the fixed point of the plain rule
     if (pass < kMaskPasses) {
       uint64_t cov = ballot(st >= ce);
       for (int it = 0; cov && it < 3; ++it) {
@@ -634,12 +637,11 @@ __device__ __attribute__((always_inline)) inline void sc_superchunk(ScLds& S, co
         if (c == cov) break;
         cov = c;
       }
-    }
-    bool chg = sn != s;
-    if (!ballot(chg)) {
-      if (!ballot(st != s)) break;  // the fixed point of the plain rule
-      sn = st;
-      chg = st != s;
+      chg = sn != s;
+      if (!ballot(chg)) {  // (the proposal changes nothing: the plain rule's starts this pass)
+        sn = st;
+        chg = st != s;
+      }
     }
 
     const bool inrow = chg && sn < ce;  // (an entry is never before the row)
